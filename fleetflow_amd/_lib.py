@@ -1,0 +1,104 @@
+"""ctypes binding of libfleetplace.so (include/fleetplace.h).
+
+The product path has NO CPU fallback: if the HIP library is missing or no gfx950
+device is present, calls raise.  The binding is the same one a Rust crate would
+declare with ``extern "C"``.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfleetplace.so")
+
+FP_OK, FP_EINVAL, FP_ENOMEM, FP_EDEVICE, FP_EOVERFLOW, FP_ECORRUPT = 0, -1, -2, -3, -4, -5
+FP_NONE = 0xFFFFFFFF
+REASON_OK, REASON_NOFIT, REASON_CYCLE = 0, 1, 2
+FP_K_PLACE, FP_K_SORT, FP_K_FEAS, FP_K_LEVEL, FP_K_GEN = 0, 1, 2, 3, 4
+
+u8p = ct.POINTER(ct.c_uint8)
+u32p = ct.POINTER(ct.c_uint32)
+u64p = ct.POINTER(ct.c_uint64)
+vp = ct.c_void_p
+
+
+class FpGraph(ct.Structure):
+    _fields_ = [("n_vertices", ct.c_uint32), ("n_edges", ct.c_uint32), ("row_ptr", vp), ("col", vp),
+                ("has_deps", vp)]
+
+
+class FpContainers(ct.Structure):
+    _fields_ = [("n", ct.c_uint32), ("cpu_m", vp), ("mem_mib", vp), ("req_labels", vp), ("conflict", vp)]
+
+
+class FpNodes(ct.Structure):
+    _fields_ = [("n", ct.c_uint32), ("cpu_free", vp), ("mem_free", vp), ("labels", vp),
+                ("conflict_used", vp), ("schedulable", vp)]
+
+
+class FpBatch(ct.Structure):
+    _fields_ = [("n_scen", ct.c_uint32), ("scen_base", ct.c_uint32), ("n_containers", ct.c_uint32),
+                ("n_nodes", ct.c_uint32),
+                ("cpu_m", vp), ("mem_mib", vp), ("req_labels", vp), ("conflict", vp), ("level", vp),
+                ("cpu_free", vp), ("mem_free", vp), ("labels", vp), ("conflict_used", vp),
+                ("schedulable", vp), ("assign", vp), ("reason", vp), ("cost", vp)]
+
+
+class FleetplaceError(RuntimeError):
+    def __init__(self, code, where):
+        self.code = code
+        msg = _lib_strerror(code) if _LIB is not None else str(code)
+        super().__init__(f"{where}: {msg} ({code})")
+
+
+_LIB = None
+
+# name -> (restype, argtypes); the full export list of include/fleetplace.h
+SIGNATURES = {
+    "fp_ctx_create": (ct.c_int, [ct.POINTER(vp), ct.c_int]),
+    "fp_ctx_destroy": (None, [vp]),
+    "fp_ctx_set_stream": (ct.c_int, [vp, vp]),
+    "fp_ctx_sync": (ct.c_int, [vp]),
+    "fp_strerror": (ct.c_char_p, [ct.c_int]),
+    "fp_abi_version": (ct.c_int, []),
+    "fp_ctx_profile": (ct.c_int, [vp, ct.c_int]),
+    "fp_ctx_kernel_stats": (ct.c_int, [vp, ct.c_int, ct.POINTER(ct.c_double), ct.POINTER(ct.c_uint64)]),
+    "fp_legacy_order": (ct.c_int, [vp, ct.POINTER(FpGraph), u32p]),
+    "fp_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), u32p, u32p, u32p]),
+    "fp_place": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p, u8p]),
+    "fp_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),
+    "fp_feasibility": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p, u64p]),
+    "fp_dev_legacy_order": (ct.c_int, [vp, ct.POINTER(FpGraph), vp]),
+    "fp_dev_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), vp, vp, vp]),
+    "fp_dev_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),
+    "fp_dev_feasibility": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), vp, vp, vp]),
+    "fp_dev_argmin_cost": (ct.c_int, [vp, vp, ct.c_uint32, vp]),
+    "fp_dev_gen_batch": (ct.c_int, [vp, ct.c_uint64, ct.POINTER(FpBatch), ct.c_uint32]),
+}
+
+
+def load():
+    """Load libfleetplace.so; raise loudly if it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback)")
+        L = ct.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _lib_strerror(code):
+    return load().fp_strerror(code).decode()
+
+
+def check(rc, where):
+    if rc != FP_OK:
+        raise FleetplaceError(rc, where)

@@ -1,0 +1,399 @@
+// fp_ctx.hip -- context lifetime, device arenas, profiling and the synchronous
+// host-pointer entry points of include/fleetplace.h.
+//
+// The host API copies caller arrays into a device staging arena, runs the same
+// device pipeline as fp_dev_*, and copies results back only when every kernel
+// succeeded ("no partial writes on error").
+#include "fp_internal.h"
+#include <string.h>
+#include <stdlib.h>
+
+int fp_hip_fail(hipError_t e) {
+    (void)e;
+    if (e == hipErrorOutOfMemory) return FP_ENOMEM;
+    return FP_EDEVICE;
+}
+
+extern "C" const char *fp_strerror(int code) {
+    switch (code) {
+    case FP_OK: return "ok";
+    case FP_EINVAL: return "invalid argument";
+    case FP_ENOMEM: return "out of memory";
+    case FP_EDEVICE: return "no gfx950 device or HIP runtime error";
+    case FP_EOVERFLOW: return "count overflow";
+    case FP_ECORRUPT: return "input violates an invariant";
+    default: return "unknown error";
+    }
+}
+
+extern "C" int fp_abi_version(void) { return FP_ABI_VERSION; }
+
+extern "C" int fp_ctx_create(fp_ctx **out, int device) {
+    if (!out) return FP_EINVAL;
+    *out = nullptr;
+    if (device < 0) return FP_EINVAL;  // no CPU backend by design
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device >= n) return FP_EDEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FP_EDEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FP_EDEVICE;
+    fp_ctx *c = new fp_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_err, 256) != hipSuccess ||
+        hipHostMalloc(&c->h_small, 4096, hipHostMallocDefault) != hipSuccess) {
+        fp_ctx_destroy(c);
+        return FP_EDEVICE;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return FP_OK;
+}
+
+extern "C" void fp_ctx_destroy(fp_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &r : c->pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (auto e : c->pool) (void)hipEventDestroy(e);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->stage) (void)hipFree(c->stage);
+    if (c->d_err) (void)hipFree(c->d_err);
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+extern "C" int fp_ctx_set_stream(fp_ctx *c, void *s) {
+    if (!c) return FP_EINVAL;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return FP_OK;
+}
+
+extern "C" int fp_ctx_sync(fp_ctx *c) {
+    if (!c) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    FP_HIP(hipStreamSynchronize(c->stream));
+    return FP_OK;
+}
+
+// ---- arenas ----------------------------------------------------------------
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+void fp_ws_reset(fp_ctx *c) { c->ws_top = 0; }
+int fp_ws_reserve(fp_ctx *c, size_t bytes) {
+    if (bytes <= c->ws_cap) return FP_OK;
+    FP_HIP(hipStreamSynchronize(c->stream));
+    if (c->ws) (void)hipFree(c->ws);
+    c->ws = nullptr;
+    c->ws_cap = 0;
+    size_t cap = align256(bytes + bytes / 4 + 4096);
+    FP_HIP(hipMalloc(&c->ws, cap));
+    c->ws_cap = cap;
+    return FP_OK;
+}
+void *fp_ws_take(fp_ctx *c, size_t bytes) {
+    size_t top = align256(c->ws_top);
+    if (top + bytes > c->ws_cap) return nullptr;
+    c->ws_top = top + bytes;
+    return c->ws + top;
+}
+void fp_stage_reset(fp_ctx *c) { c->stage_top = 0; }
+int fp_stage_reserve(fp_ctx *c, size_t bytes) {
+    if (bytes <= c->stage_cap) return FP_OK;
+    FP_HIP(hipStreamSynchronize(c->stream));
+    if (c->stage) (void)hipFree(c->stage);
+    c->stage = nullptr;
+    c->stage_cap = 0;
+    size_t cap = align256(bytes + bytes / 4 + 4096);
+    FP_HIP(hipMalloc(&c->stage, cap));
+    c->stage_cap = cap;
+    return FP_OK;
+}
+void *fp_stage_take(fp_ctx *c, size_t bytes) {
+    size_t top = align256(c->stage_top);
+    if (top + bytes > c->stage_cap) return nullptr;
+    c->stage_top = top + bytes;
+    return c->stage + top;
+}
+
+int fp_check_err(fp_ctx *c) {
+    FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    FP_HIP(hipStreamSynchronize(c->stream));
+    uint32_t e = (uint32_t)c->h_small[0];
+    if (e) return -(int)e;
+    return FP_OK;
+}
+
+// ---- profiling ---------------------------------------------------------------
+static hipEvent_t ev_get(fp_ctx *c) {
+    if (!c->pool.empty()) {
+        hipEvent_t e = c->pool.back();
+        c->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+void fp_prof_begin(fp_ctx *c, int kid, hipEvent_t *a) {
+    (void)kid;
+    *a = nullptr;
+    if (!c->profile) return;
+    *a = ev_get(c);
+    (void)hipEventRecord(*a, c->stream);
+}
+void fp_prof_end(fp_ctx *c, int kid, hipEvent_t a) {
+    if (!c->profile || !a) return;
+    hipEvent_t b = ev_get(c);
+    (void)hipEventRecord(b, c->stream);
+    c->pending.push_back({kid, a, b});
+}
+extern "C" int fp_ctx_profile(fp_ctx *c, int enable) {
+    if (!c) return FP_EINVAL;
+    c->profile = enable != 0;
+    for (int k = 0; k < FP_K_COUNT; ++k) { c->total_ms[k] = 0; c->launches[k] = 0; }
+    return FP_OK;
+}
+extern "C" int fp_ctx_kernel_stats(fp_ctx *c, int kid, double *total_ms, uint64_t *launches) {
+    if (!c || kid < 0 || kid >= FP_K_COUNT) return FP_EINVAL;
+    for (auto &r : c->pending) {
+        float ms = 0.f;
+        FP_HIP(hipEventSynchronize(r.b));
+        FP_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+        c->total_ms[r.kid] += ms;
+        c->launches[r.kid] += 1;
+        c->pool.push_back(r.a);
+        c->pool.push_back(r.b);
+    }
+    c->pending.clear();
+    if (total_ms) *total_ms = c->total_ms[kid];
+    if (launches) *launches = c->launches[kid];
+    return FP_OK;
+}
+
+// ---- device-pointer entry points ----------------------------------------------
+extern "C" int fp_dev_place_batch(fp_ctx *c, const fp_batch *b) {
+    if (!c || !b) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_dev_place_batch_impl(c, b);
+}
+extern "C" int fp_dev_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t *order,
+                               uint32_t *n_cycle_dev) {
+    if (!c || !g) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_dev_levelize_impl(c, g, level, order, n_cycle_dev);
+}
+extern "C" int fp_dev_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
+    if (!c || !g) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_dev_legacy_order_impl(c, g, perm);
+}
+extern "C" int fp_dev_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
+                                  uint32_t *first, uint32_t *count, uint64_t *bitmap) {
+    if (!c || !cs || !ns) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_dev_feasibility_impl(c, cs, ns, first, count, bitmap);
+}
+
+// ---- host-pointer entry points -------------------------------------------------
+template <class T>
+static T *stage_in(fp_ctx *c, const T *h, size_t n, int *rc) {
+    if (*rc) return nullptr;
+    if (!h) return nullptr;
+    T *d = (T *)fp_stage_take(c, n * sizeof(T) + 4);
+    if (!d) { *rc = FP_ENOMEM; return nullptr; }
+    if (n && hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        *rc = FP_EDEVICE;
+    return d;
+}
+template <class T>
+static T *stage_out(fp_ctx *c, size_t n, int *rc) {
+    if (*rc) return nullptr;
+    T *d = (T *)fp_stage_take(c, n * sizeof(T) + 4);
+    if (!d) *rc = FP_ENOMEM;
+    return d;
+}
+static int copy_back(fp_ctx *c, void *h, const void *d, size_t bytes) {
+    if (!h || !bytes) return FP_OK;
+    FP_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
+    return FP_OK;
+}
+
+extern "C" int fp_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm_out) {
+    if (!c || !g || (g->n_vertices && (!g->has_deps || !perm_out))) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    const size_t V = g->n_vertices;
+    int rc = fp_stage_reserve(c, 2 * V * 4 + 4096);
+    if (rc) return rc;
+    fp_stage_reset(c);
+    fp_graph dg = *g;
+    dg.has_deps = stage_in(c, g->has_deps, V, &rc);
+    dg.row_ptr = nullptr;
+    dg.col = nullptr;
+    uint32_t *dperm = stage_out<uint32_t>(c, V, &rc);
+    if (rc) return rc;
+    rc = fp_dev_legacy_order_impl(c, &dg, dperm);
+    if (rc) return rc;
+    if ((rc = fp_check_err(c))) return rc;
+    if ((rc = copy_back(c, perm_out, dperm, V * 4))) return rc;
+    FP_HIP(hipStreamSynchronize(c->stream));
+    return FP_OK;
+}
+
+static int validate_graph_host(const fp_graph *g) {
+    const uint32_t V = g->n_vertices;
+    if (!g->row_ptr) return FP_EINVAL;
+    if (g->row_ptr[0] != 0 || g->row_ptr[V] != g->n_edges) return FP_ECORRUPT;
+    for (uint32_t v = 0; v < V; ++v)
+        if (g->row_ptr[v + 1] < g->row_ptr[v]) return FP_ECORRUPT;
+    for (uint32_t e = 0; e < g->n_edges; ++e)
+        if (g->col[e] >= V) return FP_ECORRUPT;
+    return FP_OK;
+}
+
+extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, uint32_t *order_out,
+                           uint32_t *n_cycle_out) {
+    if (!c || !g) return FP_EINVAL;
+    const size_t V = g->n_vertices, E = g->n_edges;
+    if (V && (!g->has_deps || !g->row_ptr || !level_out || !order_out)) return FP_EINVAL;
+    if (E && !g->col) return FP_EINVAL;
+    if (V == 0) {
+        if (E) return FP_ECORRUPT;
+        if (n_cycle_out) *n_cycle_out = 0;
+        return FP_OK;
+    }
+    int rc = validate_graph_host(g);
+    if (rc) return rc;
+    FP_HIP(hipSetDevice(c->device));
+    rc = fp_stage_reserve(c, (V + 1) * 4 + E * 4 + V + 2 * V * 4 + 8 * 256);
+    if (rc) return rc;
+    fp_stage_reset(c);
+    fp_graph dg = *g;
+    dg.row_ptr = stage_in(c, g->row_ptr, V + 1, &rc);
+    dg.col = stage_in(c, g->col, E, &rc);
+    dg.has_deps = stage_in(c, g->has_deps, V, &rc);
+    uint32_t *dlev = stage_out<uint32_t>(c, V, &rc);
+    uint32_t *dord = stage_out<uint32_t>(c, V, &rc);
+    uint32_t *dcyc = stage_out<uint32_t>(c, 1, &rc);
+    if (rc) return rc;
+    rc = fp_dev_levelize_impl(c, &dg, dlev, dord, dcyc);
+    if (rc) return rc;
+    if ((rc = fp_check_err(c))) return rc;
+    if ((rc = copy_back(c, level_out, dlev, V * 4))) return rc;
+    if ((rc = copy_back(c, order_out, dord, V * 4))) return rc;
+    if (n_cycle_out && (rc = copy_back(c, n_cycle_out, dcyc, 4))) return rc;
+    FP_HIP(hipStreamSynchronize(c->stream));
+    return FP_OK;
+}
+
+static int batch_host(fp_ctx *c, const fp_batch *b) {
+    const size_t S = b->n_scen, C = b->n_containers, N = b->n_nodes;
+    const size_t SC = S * C, SN = S * N;
+    if (S && C && (!b->cpu_m || !b->mem_mib || !b->req_labels || !b->conflict || !b->assign ||
+                   !b->reason))
+        return FP_EINVAL;
+    if (S && N && (!b->cpu_free || !b->mem_free || !b->labels || !b->conflict_used ||
+                   !b->schedulable))
+        return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    int rc = fp_stage_reserve(c, SC * (4 * 6 + 1) + SN * (4 * 4 + 1) + S * 8 + 16 * 256);
+    if (rc) return rc;
+    fp_stage_reset(c);
+    fp_batch d = *b;
+    d.cpu_m = stage_in(c, b->cpu_m, SC, &rc);
+    d.mem_mib = stage_in(c, b->mem_mib, SC, &rc);
+    d.req_labels = stage_in(c, b->req_labels, SC, &rc);
+    d.conflict = stage_in(c, b->conflict, SC, &rc);
+    d.level = b->level ? stage_in(c, b->level, SC, &rc) : nullptr;
+    d.cpu_free = stage_in(c, b->cpu_free, SN, &rc);
+    d.mem_free = stage_in(c, b->mem_free, SN, &rc);
+    d.labels = stage_in(c, b->labels, SN, &rc);
+    d.conflict_used = stage_in(c, b->conflict_used, SN, &rc);
+    d.schedulable = stage_in(c, b->schedulable, SN, &rc);
+    d.assign = stage_out<uint32_t>(c, SC, &rc);
+    d.reason = stage_out<uint8_t>(c, SC, &rc);
+    d.cost = stage_out<uint64_t>(c, S, &rc);
+    if (rc) return rc;
+    rc = fp_dev_place_batch_impl(c, &d);
+    if (rc) return rc;
+    if ((rc = fp_check_err(c))) return rc;
+    if ((rc = copy_back(c, b->assign, d.assign, SC * 4))) return rc;
+    if ((rc = copy_back(c, b->reason, d.reason, SC))) return rc;
+    if (b->cost && (rc = copy_back(c, b->cost, d.cost, S * 8))) return rc;
+    if ((rc = copy_back(c, b->cpu_free, d.cpu_free, SN * 4))) return rc;
+    if ((rc = copy_back(c, b->mem_free, d.mem_free, SN * 4))) return rc;
+    if ((rc = copy_back(c, b->conflict_used, d.conflict_used, SN * 4))) return rc;
+    FP_HIP(hipStreamSynchronize(c->stream));
+    return FP_OK;
+}
+
+extern "C" int fp_place_batch(fp_ctx *c, const fp_batch *b) {
+    if (!c || !b) return FP_EINVAL;
+    return batch_host(c, b);
+}
+
+extern "C" int fp_place(fp_ctx *c, const fp_containers *cs, fp_nodes *ns, const uint32_t *level,
+                        uint32_t *assign_out, uint8_t *reason_out) {
+    if (!c || !cs || !ns) return FP_EINVAL;
+    fp_batch b;
+    memset(&b, 0, sizeof(b));
+    b.n_scen = 1;
+    b.scen_base = 0;
+    b.n_containers = cs->n;
+    b.n_nodes = ns->n;
+    b.cpu_m = cs->cpu_m;
+    b.mem_mib = cs->mem_mib;
+    b.req_labels = cs->req_labels;
+    b.conflict = cs->conflict;
+    b.level = level;
+    b.cpu_free = ns->cpu_free;
+    b.mem_free = ns->mem_free;
+    b.labels = ns->labels;
+    b.conflict_used = ns->conflict_used;
+    b.schedulable = ns->schedulable;
+    b.assign = assign_out;
+    b.reason = reason_out;
+    b.cost = nullptr;
+    return batch_host(c, &b);
+}
+
+extern "C" int fp_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
+                              uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out) {
+    if (!c || !cs || !ns) return FP_EINVAL;
+    const size_t C = cs->n, N = ns->n, WC = (C + 63) / 64;
+    if (C && (!cs->cpu_m || !cs->mem_mib || !cs->req_labels || !cs->conflict || !first_out ||
+              !count_out))
+        return FP_EINVAL;
+    if (N && (!ns->cpu_free || !ns->mem_free || !ns->labels || !ns->conflict_used ||
+              !ns->schedulable))
+        return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    int rc = fp_stage_reserve(c, C * 24 + N * 17 + (bitmap_out ? WC * N * 8 : 0) + 16 * 256);
+    if (rc) return rc;
+    fp_stage_reset(c);
+    fp_containers dc = *cs;
+    fp_nodes dn = *ns;
+    dc.cpu_m = stage_in(c, cs->cpu_m, C, &rc);
+    dc.mem_mib = stage_in(c, cs->mem_mib, C, &rc);
+    dc.req_labels = stage_in(c, cs->req_labels, C, &rc);
+    dc.conflict = stage_in(c, cs->conflict, C, &rc);
+    dn.cpu_free = stage_in(c, ns->cpu_free, N, &rc);
+    dn.mem_free = stage_in(c, ns->mem_free, N, &rc);
+    dn.labels = stage_in(c, ns->labels, N, &rc);
+    dn.conflict_used = stage_in(c, ns->conflict_used, N, &rc);
+    dn.schedulable = stage_in(c, ns->schedulable, N, &rc);
+    uint32_t *dfirst = stage_out<uint32_t>(c, C, &rc);
+    uint32_t *dcount = stage_out<uint32_t>(c, C, &rc);
+    uint64_t *dbits = bitmap_out ? stage_out<uint64_t>(c, WC * N, &rc) : nullptr;
+    if (rc) return rc;
+    rc = fp_dev_feasibility_impl(c, &dc, &dn, dfirst, dcount, dbits);
+    if (rc) return rc;
+    if ((rc = fp_check_err(c))) return rc;
+    if ((rc = copy_back(c, first_out, dfirst, C * 4))) return rc;
+    if ((rc = copy_back(c, count_out, dcount, C * 4))) return rc;
+    if (bitmap_out && (rc = copy_back(c, bitmap_out, dbits, WC * N * 8))) return rc;
+    FP_HIP(hipStreamSynchronize(c->stream));
+    return FP_OK;
+}

@@ -1,0 +1,120 @@
+// fp_feas.hip -- stage 2: containers x nodes feasibility / score sweep
+// (SURVEY.md 7.1 step 4, 8(d)).  Brute force over every (container, node) pair on
+// the given node state; node tiles are staged in LDS and read as wave-uniform
+// broadcasts while each lane owns one container.
+//
+// Outputs per container: first feasible node (FP_NONE if none), feasible-node
+// count ("score"), and optionally the feasibility bitmap, word [(c/64)*N + n],
+// bit c%64 -- exactly one wavefront ballot per node, stored coalesced.
+#include "fp_internal.h"
+
+namespace {
+
+constexpr int kBlock = 256;   // containers per block (4 waves)
+constexpr int kTile = 1024;   // nodes per LDS chunk
+
+struct alignas(16) NodeRec {
+    uint32_t cf, mf, lab, cu;
+};
+
+struct FeasArgs {
+    uint32_t C, N, WC, node_span;  // node_span: nodes per blockIdx.y (multiple of 64)
+    const uint32_t *cpu, *mem, *req, *conf;
+    const uint32_t *cf, *mf, *lab, *cu;
+    const uint8_t *sched;
+    uint32_t *first, *count;
+    uint64_t *bitmap;
+    int split;
+};
+
+__global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
+    __shared__ NodeRec rec[kTile];
+    __shared__ uint32_t sch[kTile];
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wword = (blockIdx.x * kBlock + (threadIdx.x & ~63u)) / 64;  // container word
+    const bool cin = c < a.C;
+    const uint32_t cpu = cin ? a.cpu[c] : 0xFFFFFFFFu;
+    const uint32_t mem = cin ? a.mem[c] : 0xFFFFFFFFu;
+    const uint32_t req = cin ? a.req[c] : 0u;
+    const uint32_t conf = cin ? a.conf[c] : 0u;
+    const uint32_t y0 = blockIdx.y * a.node_span;
+    const uint32_t y1 = min(a.N, y0 + a.node_span);
+    uint32_t first = FP_NONE, cnt = 0;
+    uint64_t word = 0;
+    for (uint32_t n0 = y0; n0 < y1; n0 += kTile) {
+        const uint32_t len = min((uint32_t)kTile, y1 - n0);
+        for (uint32_t i = threadIdx.x; i < len; i += kBlock) {
+            NodeRec r;
+            r.cf = a.cf[n0 + i]; r.mf = a.mf[n0 + i]; r.lab = a.lab[n0 + i]; r.cu = a.cu[n0 + i];
+            rec[i] = r;
+            sch[i] = a.sched[n0 + i];
+        }
+        __syncthreads();
+        for (uint32_t i = 0; i < len; ++i) {
+            const NodeRec r = rec[i];
+            const bool ok = cin && sch[i] && fpd::fits(cpu, mem, req, conf, r.cf, r.mf, r.lab, r.cu);
+            cnt += ok ? 1u : 0u;
+            if (ok && first == FP_NONE) first = n0 + i;
+            if (a.bitmap) {
+                const uint64_t m = __ballot(ok);
+                if (lane == (i & 63)) word = m;
+                if ((i & 63) == 63 || i + 1 == len) {
+                    const uint32_t nb = n0 + (i & ~63u);
+                    if (lane <= (i & 63) && wword < a.WC) a.bitmap[(size_t)wword * a.N + nb + lane] = word;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!cin) return;
+    if (a.split) {
+        if (first != FP_NONE) atomicMin(&a.first[c], first);
+        if (cnt) atomicAdd(&a.count[c], cnt);
+    } else {
+        a.first[c] = first;
+        a.count[c] = cnt;
+    }
+}
+
+}  // namespace
+
+int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
+                            uint32_t *first, uint32_t *count, uint64_t *bitmap) {
+    const uint32_t C = cs->n, N = ns->n;
+    if (C == 0) return FP_OK;
+    if (!cs->cpu_m || !cs->mem_mib || !cs->req_labels || !cs->conflict || !first || !count)
+        return FP_EINVAL;
+    if (N && (!ns->cpu_free || !ns->mem_free || !ns->labels || !ns->conflict_used || !ns->schedulable))
+        return FP_EINVAL;
+    hipStream_t st = c->stream;
+    FP_HIP(hipMemsetAsync(c->d_err, 0, 4, st));
+    const uint32_t xb = (C + kBlock - 1) / kBlock;
+    // split the node range over blockIdx.y until the grid is >= ~2048 blocks
+    uint32_t ysplit = 1;
+    const uint32_t max_split = N ? (N + kTile - 1) / kTile : 1;
+    while ((uint64_t)xb * ysplit < 2048 && ysplit < max_split) ysplit *= 2;
+    if (ysplit > max_split) ysplit = max_split;
+    uint32_t span = N ? (N + ysplit - 1) / ysplit : 0;
+    span = (span + 63) & ~63u;
+    if (span == 0) span = 64;
+    ysplit = N ? (N + span - 1) / span : 1;
+    FeasArgs a;
+    a.C = C; a.N = N; a.WC = (C + 63) / 64; a.node_span = span;
+    a.cpu = cs->cpu_m; a.mem = cs->mem_mib; a.req = cs->req_labels; a.conf = cs->conflict;
+    a.cf = ns->cpu_free; a.mf = ns->mem_free; a.lab = ns->labels; a.cu = ns->conflict_used;
+    a.sched = ns->schedulable;
+    a.first = first; a.count = count; a.bitmap = bitmap;
+    a.split = ysplit > 1;
+    if (a.split || N == 0) {
+        FP_HIP(hipMemsetAsync(first, 0xFF, (size_t)C * 4, st));
+        FP_HIP(hipMemsetAsync(count, 0, (size_t)C * 4, st));
+    }
+    if (N == 0) return FP_OK;
+    hipEvent_t ev;
+    fp_prof_begin(c, FP_K_FEAS, &ev);
+    k_feas<<<dim3(xb, ysplit), kBlock, 0, st>>>(a);
+    FP_HIP(hipGetLastError());
+    fp_prof_end(c, FP_K_FEAS, ev);
+    return FP_OK;
+}

@@ -1,0 +1,99 @@
+// fp_internal.h -- shared internals of libfleetplace.so (HIP, gfx950 only).
+#pragma once
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <vector>
+#include "../../include/fleetplace.h"
+
+#define FP_HIP(call)                                   \
+    do {                                               \
+        hipError_t e_ = (call);                        \
+        if (e_ != hipSuccess) return fp_hip_fail(e_);  \
+    } while (0)
+
+int fp_hip_fail(hipError_t e);
+
+struct fp_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    // kernel-side error word (e.g. a CSR index out of range): zeroed per call
+    uint32_t *d_err = nullptr;
+    // device workspace: a bump arena reset at the start of every API call
+    char *ws = nullptr;
+    size_t ws_cap = 0, ws_top = 0;
+    // host-API staging arena (device memory holding copies of host inputs)
+    char *stage = nullptr;
+    size_t stage_cap = 0, stage_top = 0;
+    // pinned host bounce buffer for small read-backs
+    uint64_t *h_small = nullptr;
+    // profiling
+    bool profile = false;
+    struct Rec { int kid; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    double total_ms[FP_K_COUNT] = {0};
+    uint64_t launches[FP_K_COUNT] = {0};
+};
+
+// arena helpers (return nullptr on failure; callers map to FP_ENOMEM)
+void fp_ws_reset(fp_ctx *c);
+int fp_ws_reserve(fp_ctx *c, size_t bytes);  // ensure capacity (may sync + realloc)
+void *fp_ws_take(fp_ctx *c, size_t bytes);   // 256-B aligned slice
+void fp_stage_reset(fp_ctx *c);
+int fp_stage_reserve(fp_ctx *c, size_t bytes);
+void *fp_stage_take(fp_ctx *c, size_t bytes);
+
+// profiling brackets around a launch on ctx->stream
+void fp_prof_begin(fp_ctx *c, int kid, hipEvent_t *a);
+void fp_prof_end(fp_ctx *c, int kid, hipEvent_t a);
+
+// kernel-side error check after a synchronising read-back
+int fp_check_err(fp_ctx *c);
+
+static inline uint32_t fp_bitwidth(uint64_t v) {
+    uint32_t b = 0;
+    while (v) { b++; v >>= 1; }
+    return b;
+}
+
+// ---- entry points shared between translation units ----
+int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b);
+int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t *order,
+                         uint32_t *n_cycle_dev);
+int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm);
+int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
+                            uint32_t *first, uint32_t *count, uint64_t *bitmap);
+
+// ---- device helpers ----
+namespace fpd {
+
+constexpr uint64_t GAMMA = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t TAG_CONT = 0xC0C0C0C0C0C0C0C0ull;
+constexpr uint64_t TAG_NODE = 0x5E5E5E5E5E5E5E5Eull;
+
+// SPEC.md 3.1: draw(seed, k) = (k+1)-th SplitMix64 output from state `seed`.
+__host__ __device__ inline uint64_t draw(uint64_t seed, uint64_t idx) {
+    uint64_t z = seed + (idx + 1) * GAMMA;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline uint64_t scenario_seed(uint64_t seed, uint32_t s) {
+    return seed ^ ((uint64_t)s * GAMMA);
+}
+
+// Single node-fit predicate (SPEC.md 2.3); sched handled by callers.
+__device__ __forceinline__ bool fits(uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
+                                     uint32_t cf, uint32_t mf, uint32_t lab, uint32_t cu) {
+    return (cf >= cpu) & (mf >= mem) & ((lab & req) == req) & ((cu & conf) == 0u);
+}
+
+__device__ __forceinline__ uint64_t pack_cost(uint32_t rej, uint32_t used, uint32_t id) {
+    uint64_t r = rej > 0xFFFFFFu ? 0xFFFFFFu : rej;
+    uint64_t u = used > 0xFFFFFFu ? 0xFFFFFFu : used;
+    return (r << 40) | (u << 16) | (uint64_t)(id & 0xFFFFu);
+}
+
+}  // namespace fpd

@@ -1,0 +1,239 @@
+"""Host-side mirror of the reference's plan-path interface.
+
+Names and argument meaning follow the Rust reference so callers (and tests) read
+the same:
+
+* ``Service`` / ``Stage`` / ``Flow``: the subset of fleetflow-core's model the
+  plan path reads (crates/fleetflow-core/src/model/service.rs:26-70,
+  model/stage.rs:48-64, model/flow.rs:15-41), plus the resource-request
+  extension of SPEC.md 4 (``cpu_m``/``mem_mib``/labels/ports/anti-affinity).
+* ``order_by_dependencies(services, flow)``: engine.rs:64-85, computed by the
+  GPU stable partition (fp_legacy_order).
+* ``resolve_target_server(flow, stage_name)``: handlers/deploy.rs:390-394,
+  computed by GPU FFD placement over the stage's servers with unconstrained
+  capacity (every container lands on node 0 == ``servers.first()``).
+* ``levelize_stage`` / ``plan_stage``: the new planner outputs (SPEC.md 2).
+
+Strings never cross the C ABI: names are mapped to u32 ids in stage order here.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .planner import NONE, Planner
+
+U32_MAX = 0xFFFFFFFF
+
+
+@dataclass
+class Service:
+    """fleetflow_core::Service subset (model/service.rs:26-70)."""
+    image: str | None = None
+    version: str | None = None
+    depends_on: list[str] = field(default_factory=list)
+    # SPEC.md 4 resource-request extension (ignored by the reference parser,
+    # parser/service.rs:222); absent => unconstrained (0)
+    cpu_m: int = 0
+    mem_mib: int = 0
+    labels: list[str] = field(default_factory=list)      # required "key=value" labels
+    host_ports: list[int] = field(default_factory=list)  # from ports{ port host=... }
+    anti_affinity: str | None = None
+
+
+@dataclass
+class Stage:
+    """fleetflow_core::Stage subset (model/stage.rs:48-64)."""
+    services: list[str] = field(default_factory=list)
+    servers: list[str] = field(default_factory=list)
+
+
+@dataclass
+class Server:
+    """Node-table entry (controlplane model.rs:399-442 capacity/labels/scheduling)."""
+    slug: str
+    cpu_m: int = U32_MAX
+    mem_mib: int = U32_MAX
+    labels: list[str] = field(default_factory=list)
+    schedulable: bool = True
+
+
+@dataclass
+class Flow:
+    """fleetflow_core::Flow subset (model/flow.rs:15-41)."""
+    name: str = ""
+    services: dict[str, Service] = field(default_factory=dict)
+    stages: dict[str, Stage] = field(default_factory=dict)
+    servers: dict[str, Server] = field(default_factory=dict)
+
+
+_PLANNER: Planner | None = None
+
+
+def default_planner() -> Planner:
+    global _PLANNER
+    if _PLANNER is None:
+        _PLANNER = Planner(0)
+    return _PLANNER
+
+
+def has_deps_vector(services: list[str], flow: Flow) -> np.ndarray:
+    """The engine.rs:71-80 predicate per position: known AND depends_on non-empty."""
+    return np.array([1 if (n in flow.services and flow.services[n].depends_on) else 0 for n in services],
+                    dtype=np.uint8)
+
+
+def order_by_dependencies(services: list[str], flow: Flow, planner: Planner | None = None) -> list[str]:
+    """engine.rs:64-85 -- same inputs, same output, computed on the GPU."""
+    if not services:
+        return []
+    p = planner or default_planner()
+    perm = p.legacy_order(has_deps_vector(services, flow))
+    return [services[i] for i in perm]
+
+
+def stage_graph(services: list[str], flow: Flow):
+    """Target set -> reversed CSR.
+
+    Vertex ids: first occurrence of each name in stage order.  Deps outside the
+    target set add no edge (they count as satisfied).  Duplicate deps give
+    duplicate edges.  Returns (vertex_names, pos_to_vertex, row_ptr, col, has_deps)."""
+    vid: dict[str, int] = {}
+    names: list[str] = []
+    pos_to_vertex = []
+    for n in services:
+        if n not in vid:
+            vid[n] = len(names)
+            names.append(n)
+        pos_to_vertex.append(vid[n])
+    V = len(names)
+    has_deps = np.zeros(V, np.uint8)
+    edges = []
+    for v, n in enumerate(names):
+        svc = flow.services.get(n)
+        if svc is None or not svc.depends_on:
+            continue
+        has_deps[v] = 1
+        for d in svc.depends_on:
+            if d in vid:
+                edges.append((vid[d], v))
+    row_ptr = np.zeros(V + 1, np.uint32)
+    for d, _ in edges:
+        row_ptr[d + 1] += 1
+    row_ptr = np.cumsum(row_ptr, dtype=np.uint64).astype(np.uint32)
+    col = np.zeros(len(edges), np.uint32)
+    fill = row_ptr[:-1].copy()
+    for d, v in edges:
+        col[fill[d]] = v
+        fill[d] += 1
+    return names, np.array(pos_to_vertex, np.uint32), row_ptr, col, has_deps
+
+
+def levelize_stage(services: list[str], flow: Flow, planner: Planner | None = None):
+    """Kahn start levels per position and the (level, position) start order."""
+    if not services:
+        return [], []
+    p = planner or default_planner()
+    names, pos2v, row_ptr, col, has_deps = stage_graph(services, flow)
+    level_v, _, _ = p.levelize(row_ptr, col, has_deps)
+    levels = [int(level_v[v]) for v in pos2v]
+    order = sorted(range(len(services)), key=lambda i: (levels[i] == NONE, levels[i], i))
+    return levels, [services[i] for i in order]
+
+
+class LabelDict:
+    """Sorted (key=value) dictionary -> bit index, <= 32 labels."""
+
+    def __init__(self, labels):
+        self.bits = {lab: i for i, lab in enumerate(sorted(set(labels)))}
+        if len(self.bits) > 32:
+            raise ValueError("more than 32 distinct labels")
+
+    def mask(self, labels):
+        m = 0
+        for lab in labels:
+            m |= 1 << self.bits[lab]
+        return m
+
+
+@dataclass
+class Plan:
+    stage: str
+    order: list[str]              # legacy-compatible start order (engine.rs:67-85)
+    levels: dict[str, int]        # Kahn levels (U32_MAX = cycle)
+    level_order: list[str]        # sort by (level, position)
+    assignment: dict[str, str]    # service -> server slug (unplaced absent)
+    rejected: dict[str, str]      # service -> "NOFIT" | "CYCLE"
+
+
+def _server_nodes(flow: Flow, servers: list[str]):
+    out = []
+    for s in servers:
+        out.append(flow.servers.get(s, Server(slug=s)))
+    return out
+
+
+def plan_stage(flow: Flow, stage_name: str, planner: Planner | None = None,
+               servers: list[Server] | None = None) -> Plan:
+    """Full planner output for one stage (SPEC.md 2)."""
+    p = planner or default_planner()
+    stage = flow.stages[stage_name]
+    services = list(stage.services)
+    order = order_by_dependencies(services, flow, p)
+    levels, level_order = levelize_stage(services, flow, p)
+    nodes = servers if servers is not None else _server_nodes(flow, stage.servers)
+    assignment, rejected = {}, {}
+    if services and nodes:
+        names, pos2v, *_ = stage_graph(services, flow)
+        lvl_v = {names[v]: levels[i] for i, v in enumerate(pos2v)}
+        svcs = [flow.services.get(n, Service()) for n in names]
+        all_labels = [lab for s in svcs for lab in s.labels] + [lab for nd in nodes for lab in nd.labels]
+        ld = LabelDict(all_labels)
+        ports = sorted({hp for s in svcs for hp in s.host_ports})
+        groups = sorted({s.anti_affinity for s in svcs if s.anti_affinity})
+        if len(ports) > 16 or len(groups) > 16:
+            raise ValueError("more than 16 host ports or anti-affinity groups in one stage")
+        pbit = {hp: i for i, hp in enumerate(ports)}
+        gbit = {g: 16 + i for i, g in enumerate(groups)}
+        cpu = [s.cpu_m for s in svcs]
+        mem = [s.mem_mib for s in svcs]
+        req = [ld.mask(s.labels) for s in svcs]
+        conf = []
+        for s in svcs:
+            m = 0
+            for hp in s.host_ports:
+                m |= 1 << pbit[hp]
+            if s.anti_affinity:
+                m |= 1 << gbit[s.anti_affinity]
+            conf.append(m)
+        cf = [nd.cpu_m for nd in nodes]
+        mf = [nd.mem_mib for nd in nodes]
+        lab = [ld.mask(nd.labels) for nd in nodes]
+        cu = [0] * len(nodes)
+        sch = [1 if nd.schedulable else 0 for nd in nodes]
+        lv = [lvl_v[n] for n in names]
+        assign, reason, _ = p.place((cpu, mem, req, conf), (cf, mf, lab, cu, sch), level=lv)
+        for v, n in enumerate(names):
+            if assign[v] != NONE:
+                assignment[n] = nodes[assign[v]].slug
+            else:
+                rejected[n] = "CYCLE" if reason[v] == 2 else "NOFIT"
+    return Plan(stage_name, order, dict(zip(services, levels)), level_order, assignment, rejected)
+
+
+def resolve_target_server(flow: Flow, stage_name: str, planner: Planner | None = None) -> str | None:
+    """handlers/deploy.rs:390-394: ``flow.stages.get(stage).and_then(|s| s.servers.first().cloned())``.
+
+    Computed as FFD over the stage's servers with unconstrained capacity: every
+    service lands on node 0.  An empty or missing stage/server list gives None
+    (the caller records "local", :396-398)."""
+    stage = flow.stages.get(stage_name)
+    if stage is None or not stage.servers:
+        return None
+    p = planner or default_planner()
+    n = max(1, len(stage.services))
+    nodes = ([U32_MAX] * len(stage.servers), [U32_MAX] * len(stage.servers), [0] * len(stage.servers),
+             [0] * len(stage.servers), [1] * len(stage.servers))
+    assign, _, _ = p.place(([0] * n, [0] * n, [0] * n, [0] * n), nodes)
+    return stage.servers[int(assign[0])]

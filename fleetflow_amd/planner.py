@@ -1,0 +1,220 @@
+"""Host-side wrappers over the C ABI (include/fleetplace.h).
+
+``Planner`` owns one ``fp_ctx`` (one HIP stream on one MI355X).  The numpy
+methods use the synchronous host-pointer entry points (the drop-in boundary a
+Rust/cgo caller would use); ``DevBatch`` + the ``dev_*`` methods run the same
+kernels on device-resident tensors (torch is only the HBM allocator here).
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import FpBatch, FpContainers, FpGraph, FpNodes, check
+
+NONE = _lib.FP_NONE
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _u8(a):
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class Planner:
+    def __init__(self, device: int = 0):
+        self._L = _lib.load()
+        h = ct.c_void_p()
+        check(self._L.fp_ctx_create(ct.byref(h), device), "fp_ctx_create")
+        self._ctx = h
+        self.device = device
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.fp_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_stream(self, hip_stream_handle: int | None):
+        check(self._L.fp_ctx_set_stream(self._ctx, hip_stream_handle or None), "fp_ctx_set_stream")
+
+    def sync(self):
+        check(self._L.fp_ctx_sync(self._ctx), "fp_ctx_sync")
+
+    def profile(self, enable=True):
+        check(self._L.fp_ctx_profile(self._ctx, int(enable)), "fp_ctx_profile")
+
+    def kernel_stats(self, kernel_id: int):
+        ms = ct.c_double()
+        n = ct.c_uint64()
+        check(self._L.fp_ctx_kernel_stats(self._ctx, kernel_id, ct.byref(ms), ct.byref(n)), "kernel_stats")
+        return ms.value, n.value
+
+    # -- host-pointer API ------------------------------------------------------------
+    def legacy_order(self, has_deps):
+        """engine.rs:67-85 on indices: has_deps[i] = known && depends_on non-empty."""
+        hd = _u8(has_deps)
+        out = np.empty(hd.size, np.uint32)
+        g = FpGraph(hd.size, 0, None, None, _ptr(hd))
+        check(self._L.fp_legacy_order(self._ctx, ct.byref(g), out.ctypes.data_as(_lib.u32p)), "fp_legacy_order")
+        return out
+
+    def levelize(self, row_ptr, col, has_deps):
+        rp, cl, hd = _u32(row_ptr), _u32(col), _u8(has_deps)
+        V = hd.size
+        level = np.empty(V, np.uint32)
+        order = np.empty(V, np.uint32)
+        ncyc = ct.c_uint32()
+        g = FpGraph(V, cl.size, _ptr(rp), _ptr(cl) if cl.size else None, _ptr(hd))
+        check(self._L.fp_levelize(self._ctx, ct.byref(g), level.ctypes.data_as(_lib.u32p),
+                                  order.ctypes.data_as(_lib.u32p), ct.byref(ncyc)), "fp_levelize")
+        return level, order, ncyc.value
+
+    def place(self, cont, nodes, level=None):
+        """cont = (cpu_m, mem_mib, req_labels, conflict); nodes = (cpu_free, mem_free,
+        labels, conflict_used, schedulable).  Inputs are not mutated; the updated node
+        state is returned.  Returns (assign, reason, nodes_after)."""
+        cpu, mem, req, conf = (_u32(x) for x in cont)
+        cf, mf = _u32(nodes[0]).copy(), _u32(nodes[1]).copy()
+        lab, cu, sched = _u32(nodes[2]), _u32(nodes[3]).copy(), _u8(nodes[4])
+        C, N = cpu.size, cf.size
+        assign = np.empty(C, np.uint32)
+        reason = np.empty(C, np.uint8)
+        lv = _u32(level) if level is not None else None
+        cs = FpContainers(C, _ptr(cpu), _ptr(mem), _ptr(req), _ptr(conf))
+        ns = FpNodes(N, _ptr(cf), _ptr(mf), _ptr(lab), _ptr(cu), _ptr(sched))
+        check(self._L.fp_place(self._ctx, ct.byref(cs), ct.byref(ns),
+                               lv.ctypes.data_as(_lib.u32p) if lv is not None else None,
+                               assign.ctypes.data_as(_lib.u32p), reason.ctypes.data_as(_lib.u8p)), "fp_place")
+        return assign, reason, (cf, mf, lab, cu, sched)
+
+    def place_batch(self, S, C, N, cont, nodes, level=None, scen_base=0):
+        """Scenario-major arrays ([S*C] containers, [S*N] nodes).  Returns
+        (assign, reason, cost, nodes_after)."""
+        cpu, mem, req, conf = (_u32(x) for x in cont)
+        cf, mf = _u32(nodes[0]).copy(), _u32(nodes[1]).copy()
+        lab, cu, sched = _u32(nodes[2]), _u32(nodes[3]).copy(), _u8(nodes[4])
+        assert cpu.size == S * C and cf.size == S * N
+        lv = _u32(level) if level is not None else None
+        assign = np.empty(S * C, np.uint32)
+        reason = np.empty(S * C, np.uint8)
+        cost = np.empty(S, np.uint64)
+        b = FpBatch(S, scen_base, C, N, _ptr(cpu), _ptr(mem), _ptr(req), _ptr(conf), _ptr(lv), _ptr(cf),
+                    _ptr(mf), _ptr(lab), _ptr(cu), _ptr(sched), _ptr(assign), _ptr(reason), _ptr(cost))
+        check(self._L.fp_place_batch(self._ctx, ct.byref(b)), "fp_place_batch")
+        return assign, reason, cost, (cf, mf, lab, cu, sched)
+
+    def feasibility(self, cont, nodes, bitmap=True):
+        cpu, mem, req, conf = (_u32(x) for x in cont)
+        cf, mf, lab, cu = (_u32(x) for x in nodes[:4])
+        sched = _u8(nodes[4])
+        C, N = cpu.size, cf.size
+        first = np.empty(C, np.uint32)
+        count = np.empty(C, np.uint32)
+        bm = np.empty(((C + 63) // 64) * N, np.uint64) if bitmap else None
+        cs = FpContainers(C, _ptr(cpu), _ptr(mem), _ptr(req), _ptr(conf))
+        ns = FpNodes(N, _ptr(cf), _ptr(mf), _ptr(lab), _ptr(cu), _ptr(sched))
+        check(self._L.fp_feasibility(self._ctx, ct.byref(cs), ct.byref(ns), first.ctypes.data_as(_lib.u32p),
+                                     count.ctypes.data_as(_lib.u32p),
+                                     bm.ctypes.data_as(_lib.u64p) if bm is not None else None), "fp_feasibility")
+        return first, count, bm
+
+    # -- device-pointer API -------------------------------------------------------------
+    def dev_gen_batch(self, seed, db: "DevBatch", flags=7):
+        check(self._L.fp_dev_gen_batch(self._ctx, ct.c_uint64(seed), ct.byref(db.struct()), flags),
+              "fp_dev_gen_batch")
+
+    def dev_place_batch(self, db: "DevBatch"):
+        check(self._L.fp_dev_place_batch(self._ctx, ct.byref(db.struct())), "fp_dev_place_batch")
+
+    def dev_argmin_cost(self, cost_t, out_t):
+        check(self._L.fp_dev_argmin_cost(self._ctx, cost_t.data_ptr(), cost_t.numel(), out_t.data_ptr()),
+              "fp_dev_argmin_cost")
+
+    def dev_feasibility(self, db: "DevBatch", first_t, count_t, bitmap_t=None, scenario=0):
+        C, N = db.C, db.N
+        o, p = scenario * C, scenario * N
+        cs = FpContainers(C, db.cpu[o:].data_ptr(), db.mem[o:].data_ptr(), db.req[o:].data_ptr(),
+                          db.conf[o:].data_ptr())
+        ns = FpNodes(N, db.cf[p:].data_ptr(), db.mf[p:].data_ptr(), db.lab[p:].data_ptr(), db.cu[p:].data_ptr(),
+                     db.sched[p:].data_ptr())
+        check(self._L.fp_dev_feasibility(self._ctx, ct.byref(cs), ct.byref(ns), first_t.data_ptr(),
+                                         count_t.data_ptr(), bitmap_t.data_ptr() if bitmap_t is not None else None),
+              "fp_dev_feasibility")
+
+    def dev_levelize(self, row_ptr_t, col_t, has_deps_t, level_t, order_t, ncyc_t):
+        V = has_deps_t.numel()
+        g = FpGraph(V, col_t.numel(), row_ptr_t.data_ptr(), col_t.data_ptr() if col_t.numel() else None,
+                    has_deps_t.data_ptr())
+        check(self._L.fp_dev_levelize(self._ctx, ct.byref(g), level_t.data_ptr(), order_t.data_ptr(),
+                                      ncyc_t.data_ptr()), "fp_dev_levelize")
+
+
+@dataclass
+class DevBatch:
+    """Device-resident scenario batch (torch tensors on one GPU, int32 storage
+    reinterpreted as uint32 by the kernels)."""
+    S: int
+    C: int
+    N: int
+    scen_base: int
+    cpu: object
+    mem: object
+    req: object
+    conf: object
+    level: object
+    cf: object
+    mf: object
+    lab: object
+    cu: object
+    sched: object
+    assign: object
+    reason: object
+    cost: object
+
+    @classmethod
+    def allocate(cls, S, C, N, device, scen_base=0, with_level=False):
+        import torch
+
+        def i32(n):
+            return torch.empty(n, dtype=torch.int32, device=device)
+
+        return cls(S, C, N, scen_base, i32(S * C), i32(S * C), i32(S * C), i32(S * C),
+                   i32(S * C) if with_level else None, i32(S * N), i32(S * N), i32(S * N), i32(S * N),
+                   torch.empty(S * N, dtype=torch.uint8, device=device), i32(S * C),
+                   torch.empty(S * C, dtype=torch.uint8, device=device),
+                   torch.empty(S, dtype=torch.int64, device=device))
+
+    def struct(self):
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        return FpBatch(self.S, self.scen_base, self.C, self.N, p(self.cpu), p(self.mem), p(self.req),
+                       p(self.conf), p(self.level), p(self.cf), p(self.mf), p(self.lab), p(self.cu),
+                       p(self.sched), p(self.assign), p(self.reason), p(self.cost))
+
+    def node_snapshot(self):
+        return tuple(t.clone() for t in (self.cf, self.mf, self.lab, self.cu, self.sched))
+
+    def restore_nodes(self, snap):
+        for dst, src in zip((self.cf, self.mf, self.lab, self.cu, self.sched), snap):
+            dst.copy_(src)

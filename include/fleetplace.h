@@ -1,0 +1,147 @@
+/*
+ * fleetplace.h -- C ABI of the MI355X-native FleetFlow placement planner
+ * (libfleetplace.so, HIP/gfx950).  This is the drop-in boundary for the
+ * reference's plan path.
+ *
+ * Reference interfaces this ABI replaces (paths relative to chronista-club/fleetflow):
+ *   fp_legacy_order   <- fn order_by_dependencies(&[String], &Flow) -> Vec<String>
+ *                        crates/fleetflow-container/src/engine.rs:64-85
+ *                        (names -> u32 ids in stage order are mapped by the caller;
+ *                         strings never cross this ABI)
+ *   fp_levelize       <- new: Kahn start levels generalising engine.rs:67-85
+ *                        (replaces the call at engine.rs:157 when levels are wanted)
+ *   fp_place          <- `stages[stage].servers.first()` with "local" fallback
+ *                        crates/fleetflow-controlplane/src/handlers/deploy.rs:386-398
+ *                        (N = 1, unconstrained capacity reproduces it exactly)
+ *   fp_place_batch    <- new: what-if scenarios, one plan per scenario + packed cost
+ *   fp_feasibility    <- new: stage-2 containers x nodes feasibility/score sweep
+ *
+ * Conventions
+ *   - All buffers are caller-owned; no allocation crosses the ABI.
+ *   - fp_* take HOST pointers and are synchronous: on error nothing is written.
+ *   - fp_dev_* take DEVICE (HBM) pointers of the context's device and are
+ *     asynchronous on the context's stream; fp_ctx_sync() reports kernel errors.
+ *   - Return 0 (FP_OK) or a negative FP_E* code.  There is no CPU fallback:
+ *     fp_ctx_create fails with FP_EDEVICE when no MI355X (gfx950) is present.
+ *   - One fp_ctx per host thread; contexts are not shared.
+ *   - Integer semantics only; results are bit-exact with the CPU oracle
+ *     (oracle/fp_oracle.c) by construction.  Semantics: SPEC.md.
+ */
+#ifndef FLEETPLACE_H
+#define FLEETPLACE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FP_ABI_VERSION 1
+
+#define FP_OK 0
+#define FP_EINVAL (-1)     /* bad argument / inconsistent sizes                  */
+#define FP_ENOMEM (-2)     /* device or host allocation failed                   */
+#define FP_EDEVICE (-3)    /* no gfx950 device, or a HIP runtime error           */
+#define FP_EOVERFLOW (-4)  /* a count exceeds uint32 / a packed-cost field       */
+#define FP_ECORRUPT (-5)   /* input violates an invariant (e.g. CSR col >= V)    */
+
+#define FP_NONE 0xFFFFFFFFu /* "no node" / "no level" (cycle)                    */
+
+enum fp_reason { FP_REASON_OK = 0, FP_REASON_NOFIT = 1, FP_REASON_CYCLE = 2 };
+
+typedef struct fp_ctx fp_ctx;
+
+/* depends_on graph as a REVERSED CSR: row d lists the vertices that depend on d.
+ * has_deps[v] = 1 iff v is known in flow.services and its depends_on is non-empty
+ * (the engine.rs:71-80 predicate). */
+typedef struct {
+    uint32_t n_vertices, n_edges;
+    const uint32_t *row_ptr;  /* [n_vertices + 1] */
+    const uint32_t *col;      /* [n_edges]        */
+    const uint8_t *has_deps;  /* [n_vertices]     */
+} fp_graph;
+
+/* Container requests, SoA: integer CPU millicores, memory MiB, required label
+ * bits, conflict bits (host-port bits | anti-affinity group bits). */
+typedef struct {
+    uint32_t n;
+    const uint32_t *cpu_m, *mem_mib, *req_labels, *conflict;
+} fp_containers;
+
+/* Node table, SoA, in node-index order (stage.servers order for KDL input,
+ * ORDER BY slug for the controlplane registry, db.rs:741-750).  cpu_free,
+ * mem_free and conflict_used are updated in place by placement. */
+typedef struct {
+    uint32_t n;
+    uint32_t *cpu_free, *mem_free;
+    const uint32_t *labels;
+    uint32_t *conflict_used;
+    const uint8_t *schedulable; /* 0 = cordon/drain (model.rs:435-442) */
+} fp_nodes;
+
+/* S independent what-if scenarios, each C containers on its own N nodes.
+ * Every array is scenario-major: container arrays [S][C], node arrays [S][N]. */
+typedef struct {
+    uint32_t n_scen, scen_base;   /* scen_base: global id of scenario 0 (cost field) */
+    uint32_t n_containers, n_nodes;
+    const uint32_t *cpu_m, *mem_mib, *req_labels, *conflict;
+    const uint32_t *level;        /* [S][C] or NULL: FP_NONE => CYCLE, not placed   */
+    uint32_t *cpu_free, *mem_free;
+    const uint32_t *labels;
+    uint32_t *conflict_used;
+    const uint8_t *schedulable;
+    uint32_t *assign;             /* [S][C] node index or FP_NONE                   */
+    uint8_t *reason;              /* [S][C] enum fp_reason                          */
+    uint64_t *cost;               /* [S] (n_rejected:24 | n_nodes_used:24 | id:16)  */
+} fp_batch;
+
+/* ---- context ------------------------------------------------------------ */
+int fp_ctx_create(fp_ctx **out, int device);
+void fp_ctx_destroy(fp_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int fp_ctx_set_stream(fp_ctx *ctx, void *hip_stream);
+int fp_ctx_sync(fp_ctx *ctx);
+const char *fp_strerror(int code);
+int fp_abi_version(void);
+/* Kernel timing (HIP events on the launch stream) for the roofline report.
+ * kernel ids: see FP_K_* below. */
+enum { FP_K_PLACE = 0, FP_K_SORT = 1, FP_K_FEAS = 2, FP_K_LEVEL = 3, FP_K_GEN = 4, FP_K_COUNT = 5 };
+int fp_ctx_profile(fp_ctx *ctx, int enable);
+int fp_ctx_kernel_stats(fp_ctx *ctx, int kernel_id, double *total_ms, uint64_t *launches);
+
+/* ---- host-pointer API (drop-in, synchronous) ---------------------------- */
+/* A1 engine.rs:67-85: perm_out = stable partition (has_deps == 0 first). */
+int fp_legacy_order(fp_ctx *ctx, const fp_graph *g, uint32_t *perm_out);
+/* A2: level_out[v] (FP_NONE on/after a cycle), order_out = sort by (level, index).
+ * n_cycle_out (nullable) receives the number of FP_NONE vertices. */
+int fp_levelize(fp_ctx *ctx, const fp_graph *g, uint32_t *level_out, uint32_t *order_out,
+                uint32_t *n_cycle_out);
+/* A6: first-fit-decreasing; nodes mutated in place; level nullable. */
+int fp_place(fp_ctx *ctx, const fp_containers *c, fp_nodes *nodes, const uint32_t *level,
+             uint32_t *assign_out, uint8_t *reason_out);
+int fp_place_batch(fp_ctx *ctx, const fp_batch *b);
+/* Stage 2: first feasible node (FP_NONE) and feasible-node count per container on
+ * the given node state; bitmap_out (nullable, ceil(C/64) * N words) holds
+ * bit (c, n) at word [(c/64) * N + n], bit c % 64. */
+int fp_feasibility(fp_ctx *ctx, const fp_containers *c, const fp_nodes *nodes,
+                   uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out);
+
+/* ---- device-pointer API (async on the ctx stream) ----------------------- */
+int fp_dev_legacy_order(fp_ctx *ctx, const fp_graph *g, uint32_t *perm_out);
+int fp_dev_levelize(fp_ctx *ctx, const fp_graph *g, uint32_t *level_out, uint32_t *order_out,
+                    uint32_t *n_cycle_out_dev);
+int fp_dev_place_batch(fp_ctx *ctx, const fp_batch *b);
+int fp_dev_feasibility(fp_ctx *ctx, const fp_containers *c, const fp_nodes *nodes,
+                       uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out);
+/* Best plan over a cost vector (device): writes the argmin index to *best_dev. */
+int fp_dev_argmin_cost(fp_ctx *ctx, const uint64_t *cost, uint32_t n, uint32_t *best_dev);
+
+/* ---- synthetic inputs (SPEC.md section 3), device-side ------------------- */
+/* flags: bit0 host ports, bit1 anti-affinity groups, bit2 required labels. */
+int fp_dev_gen_batch(fp_ctx *ctx, uint64_t seed, const fp_batch *b, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,224 @@
+"""GPU parity: every HIP path, called through the C ABI, is bit-exact with the CPU
+oracle on the same seeded inputs, the reference's known answers and the golden
+fixtures; full-size configs are checked through size-independent invariants."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NONE = 0xFFFFFFFF
+SEED = 0x5EED0000
+
+
+def _flow(case):
+    from fleetflow_amd.flow import Flow, Service
+    return Flow(services={n: Service(depends_on=d) for n, d in case["depends_on"].items()})
+
+
+# ---- A1 legacy order ----------------------------------------------------------------
+def test_order_by_dependencies_reference_kats(kats, planner):
+    from fleetflow_amd.flow import order_by_dependencies
+    for case in kats["order_by_dependencies"]:
+        assert order_by_dependencies(case["services"], _flow(case), planner) == case["expected"], case["source"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1023, 1024, 1025, 100_000, 1_000_000])
+def test_legacy_order_random(n, planner, O):
+    rng = np.random.default_rng(n)
+    hd = (rng.random(n) < 0.37).astype(np.uint8)
+    if n == 0:
+        assert planner.legacy_order(hd).size == 0
+        return
+    assert np.array_equal(planner.legacy_order(hd), O.legacy_order(hd))
+
+
+# ---- A2 levels -----------------------------------------------------------------------
+def test_levels_known_answers(kats, planner):
+    from fleetflow_amd.flow import levelize_stage
+    for case in kats["levels_expected"]:
+        levels, order = levelize_stage(case["services"], _flow(case), planner)
+        assert levels == case["levels"], case["source"]
+        assert order == case["level_order"], case["source"]
+
+
+def test_levelize_golden(golden, planner):
+    for case in golden["levelize"]:
+        level, order, ncyc = planner.levelize(case["row_ptr"], case["col"], case["has_deps"])
+        assert level.tolist() == case["level"] and order.tolist() == case["order"]
+        assert ncyc == sum(1 for x in case["level"] if x == NONE)
+
+
+@pytest.mark.parametrize("params", [(20, 30, 6, 50, 3), (0, 0, 4, 100, 5), (200, 3, 2, 300, 0), (1, 1, 0, 0, 0)])
+def test_levelize_random_dags(params, planner, O):
+    rp, col, hd = O.gen_dag(SEED + sum(params), *params)
+    level, order, ncyc = planner.levelize(rp, col, hd)
+    el, eo, en = O.levelize(rp, col, hd)
+    assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
+def test_levelize_config5_full_size(planner, O):
+    """BASELINE config 5: 1M vertices (1000 chains x 500 + 50 layers x 10k), 333 3-cycles."""
+    rp, col, hd = O.gen_dag(SEED + 5, 1000, 500, 50, 10_000, 333)
+    level, order, ncyc = planner.levelize(rp, col, hd)
+    el, eo, en = O.levelize(rp, col, hd)
+    assert ncyc == en == 999
+    assert np.array_equal(level, el) and np.array_equal(order, eo)
+
+
+def test_levelize_rejects_corrupt_csr(planner):
+    from fleetflow_amd._lib import FleetplaceError
+    with pytest.raises(FleetplaceError):
+        planner.levelize([0, 1, 2], [0, 7], [0, 1])      # col out of range
+    with pytest.raises(FleetplaceError):
+        planner.levelize([0, 2, 1], [1, 0], [0, 1])      # row_ptr not monotone
+
+
+# ---- A5 static server resolution / config 1 ----------------------------------------------
+def test_resolve_target_server_kats(kats, planner):
+    from fleetflow_amd.flow import Flow, Service, Stage, resolve_target_server
+    for case in kats["resolve_target_server"]:
+        flow = Flow(services={s: Service() for s in case["services"]},
+                    stages={"live": Stage(services=case["services"], servers=case["servers"])})
+        assert resolve_target_server(flow, "live", planner) == case["expected"], case["source"]
+    assert resolve_target_server(Flow(), "missing", planner) is None
+
+
+def test_dry_run_fixtures(kats, planner):
+    from fleetflow_amd.flow import Flow, Service, Stage, plan_stage
+    for fx in kats["dry_run_fixtures"]:
+        flow = Flow(services={n: Service(depends_on=d) for n, d in fx["depends_on"].items()},
+                    stages={fx["stage"]: Stage(services=fx["services"], servers=fx["servers"])})
+        plan = plan_stage(flow, fx["stage"], planner)
+        assert plan.order == fx["order"]
+        assert [plan.levels[s] for s in fx["services"]] == fx["levels"]
+        assert plan.assignment == {} and plan.rejected == {}  # no servers -> "local"
+
+
+# ---- A6 FFD ------------------------------------------------------------------------------
+def test_ffd_golden(golden, planner, O):
+    for case in golden["ffd"]:
+        s = O.scenario_seed(case["seed"], case["scenario"])
+        cont = O.gen_containers(s, case["C"], case["flags"])
+        nodes = O.gen_nodes(s, case["N"])
+        assign, reason, after = planner.place(cont, nodes, level=case["level"])
+        assert assign.tolist() == case["assign"], case["name"]
+        assert reason.tolist() == case["reason"], case["name"]
+        assert [after[0].tolist(), after[1].tolist(), after[3].tolist()] == case["nodes_after"]
+
+
+def _check_ffd(planner, O, cont, nodes, level=None):
+    assign, reason, after = planner.place(cont, nodes, level=level)
+    ea, er, eafter, _ = O.place(cont, nodes, level=level)
+    assert np.array_equal(assign, ea)
+    assert np.array_equal(reason, er)
+    for i in (0, 1, 3):
+        assert np.array_equal(after[i], eafter[i])
+    return assign, reason
+
+
+@pytest.mark.parametrize("C,N,flags", [(1, 1, 7), (64, 64, 7), (65, 63, 7), (1000, 100, 7), (3000, 300, 1),
+                                       (2000, 9500, 7), (1500, 12_000, 7)])
+def test_ffd_random_vs_oracle(C, N, flags, planner, O):
+    cont, nodes = O.gen_scenario(SEED + C + N, 0, C, N, flags)
+    _check_ffd(planner, O, cont, nodes)
+
+
+def test_ffd_edge_cases(planner, O):
+    rng = np.random.default_rng(1)
+    # zero-demand containers must not land on unschedulable nodes; req labels; conflicts
+    C, N = 300, 50
+    cont = (np.zeros(C, np.uint32), np.zeros(C, np.uint32), rng.integers(0, 4, C).astype(np.uint32),
+            (1 << rng.integers(0, 32, C)).astype(np.uint32) * (rng.random(C) < 0.5))
+    nodes = (rng.integers(0, 5, N).astype(np.uint32), rng.integers(0, 5, N).astype(np.uint32),
+             rng.integers(0, 4, N).astype(np.uint32), np.zeros(N, np.uint32),
+             (rng.random(N) < 0.6).astype(np.uint8))
+    _check_ffd(planner, O, cont, nodes)
+    # no nodes at all: everything NOFIT
+    a, r, _ = planner.place(([5, 6], [1, 1], [0, 0], [0, 0]), ([], [], [], [], []))
+    assert a.tolist() == [NONE, NONE] and r.tolist() == [1, 1]
+    # no containers
+    a, r, _ = planner.place(([], [], [], []), ([1], [1], [0], [0], [1]))
+    assert a.size == 0
+    # cycles are not placed
+    a, r, _ = planner.place(([1, 1, 1], [1, 1, 1], [0, 0, 0], [0, 0, 0]), ([9], [9], [0], [0], [1]),
+                            level=[0, NONE, 1])
+    assert a.tolist() == [0, NONE, 0] and r.tolist() == [0, 2, 0]
+    # max-value fields (full u32 range)
+    big = 0xFFFFFFFF
+    _check_ffd(planner, O, ([big, big - 1, 0], [big, 0, big], [big, 0, 1], [big, 0, 0]),
+               ([big, big], [big, big], [big, 1], [0, 0], [1, 1]))
+
+
+def test_ffd_batch_vs_oracle(planner, O):
+    S, C, N, flags, base = 7, 700, 90, 7, 100
+    conts, nodes = [], []
+    for s in range(S):
+        c, n = O.gen_scenario(SEED, base + s, C, N, flags)
+        conts.append(c)
+        nodes.append(n)
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    assign, reason, cost, after = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
+                                                      [cat(nodes, i) for i in range(5)], scen_base=base)
+    for s in range(S):
+        ea, er, eafter, _ = O.place(conts[s], nodes[s])
+        assert np.array_equal(assign[s * C:(s + 1) * C], ea)
+        assert np.array_equal(reason[s * C:(s + 1) * C], er)
+        assert int(cost[s]) == O.cost(ea, N, base + s)
+        assert np.array_equal(after[0][s * N:(s + 1) * N], eafter[0])
+
+
+def test_config2_full_size(planner, O):
+    """BASELINE config 2: 10k services x 1k servers, cpu/mem/port constraints."""
+    cont, nodes = O.gen_scenario(SEED + 2, 0, 10_000, 1_000, 1)
+    _check_ffd(planner, O, cont, nodes)
+
+
+def test_config4_scenarios_full_size(planner, O):
+    """BASELINE config 4 shape (50k x 5k per scenario), a few scenarios, via the device API."""
+    import torch
+    from fleetflow_amd import DevBatch
+    S, C, N, base = 3, 50_000, 5_000, 4093
+    db = DevBatch.allocate(S, C, N, "cuda:0", scen_base=base)
+    planner.dev_gen_batch(SEED + 4, db, 7)
+    torch.cuda.synchronize()
+    for s in range(S):  # device generator == oracle generator
+        ec, en = O.gen_scenario(SEED + 4, base + s, C, N, 7)
+        got = [t[s * C:(s + 1) * C].cpu().numpy().view(np.uint32) for t in (db.cpu, db.mem, db.req, db.conf)]
+        assert all(np.array_equal(g, e) for g, e in zip(got, ec))
+        gn = [t[s * N:(s + 1) * N].cpu().numpy() for t in (db.cf, db.mf, db.lab, db.cu, db.sched)]
+        assert all(np.array_equal(g.view(e.dtype), e) for g, e in zip(gn, en))
+    planner.dev_place_batch(db)
+    planner.sync()
+    for s in range(S):
+        ec, en = O.gen_scenario(SEED + 4, base + s, C, N, 7)
+        ea, er, eafter, _ = O.place(ec, en)
+        assert np.array_equal(db.assign[s * C:(s + 1) * C].cpu().numpy().view(np.uint32), ea)
+        assert np.array_equal(db.reason[s * C:(s + 1) * C].cpu().numpy(), er)
+        assert int(db.cost[s].item()) == O.cost(ea, N, base + s)
+    best = torch.empty(1, dtype=torch.int32, device="cuda:0")
+    planner.dev_argmin_cost(db.cost, best)
+    costs = [int(x) for x in db.cost.cpu().numpy().view(np.uint64)]
+    assert int(best.item()) == int(np.argmin(costs))
+
+
+# ---- stage 2 feasibility --------------------------------------------------------------------
+def test_feasibility_golden(golden, planner, O):
+    for case in golden["feasibility"]:
+        s = O.scenario_seed(case["seed"], 0)
+        cont = O.gen_containers(s, case["C"], case["flags"])
+        nodes = O.gen_nodes(s, case["N"])
+        first, count, bm = planner.feasibility(cont, nodes)
+        assert first.tolist() == case["first"] and count.tolist() == case["count"]
+        assert [f"{int(w):016x}" for w in bm] == case["bitmap_hex"]
+
+
+@pytest.mark.parametrize("C,N", [(1, 1), (200, 5000), (5000, 200), (64, 70_000), (3333, 3333)])
+def test_feasibility_random_vs_oracle(C, N, planner, O):
+    cont, nodes = O.gen_scenario(SEED + 7 * C + N, 1, C, N, 7)
+    rng = np.random.default_rng(C)
+    cf = nodes[0] - rng.integers(0, 3000, N).clip(0, nodes[0]).astype(np.uint32)
+    cu = (rng.random(N) < 0.3).astype(np.uint32) << rng.integers(0, 32, N).astype(np.uint32)
+    nodes = (cf, nodes[1], nodes[2], cu, nodes[4])
+    first, count, bm = planner.feasibility(cont, nodes)
+    ef, ec, eb = O.feasibility(cont, nodes)
+    assert np.array_equal(first, ef) and np.array_equal(count, ec) and np.array_equal(bm, eb)
