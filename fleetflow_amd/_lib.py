@@ -82,6 +82,15 @@ def load():
     """Load libfleetplace.so; raise loudly if it has not been built."""
     global _LIB
     if _LIB is None:
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7.
+        # Loading torch first makes our DT_NEEDED libamdhip64.so.7 bind to that same
+        # runtime (same SONAME), so device pointers from torch tensors and from this
+        # library live in one HIP context.  Loading ours first would leave torch with
+        # a second runtime that finds no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

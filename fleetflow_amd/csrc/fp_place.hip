@@ -245,7 +245,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
                                                (uint64_t *)nullptr, (uint32_t *)nullptr,
                                                (uint32_t *)nullptr, (unsigned)SC, S,
                                                (uint32_t *)nullptr, (uint32_t *)nullptr, 0, 64, st));
-    const size_t need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + 16 * 256;
+    const size_t need = SC * (8 * 2 + 4 * 2 + 4 * 5) + (S + 1) * 4 + sort_tmp + 24 * 256;
     int rc = fp_ws_reserve(c, need);
     if (rc) return rc;
     fp_ws_reset(c);
@@ -292,6 +292,10 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     fp_prof_end(c, FP_K_SORT, ev);
 
     // ---- 4: placement ----
+    uint32_t pG, pW;
+    size_t plds;
+    if (fp_pipe_plan(N, &pG, &pW, &plds))
+        return fp_pipe_launch(c, S, C, N, b->scen_base, order, b, maxc, maxm);
     FfdArgs a;
     a.S = S; a.C = C; a.N = N; a.scen_base = b->scen_base;
     a.cpu = b->cpu_m; a.mem = b->mem_mib; a.req = b->req_labels; a.conf = b->conflict;
