@@ -94,7 +94,9 @@ def main():
     S = args.scenarios_per_gpu
     C, N = C_PER_SCEN, N_PER_SCEN
     planner = Planner(local_rank)
-    stream = torch.cuda.current_stream(dev)
+    # one dedicated stream for torch's copies/collectives AND the planner kernels
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     planner.set_stream(stream.cuda_stream)
     db = DevBatch.allocate(S, C, N, dev, scen_base=rank * S)
     planner.dev_gen_batch(SEED, db, FLAGS)
@@ -111,9 +113,11 @@ def main():
         else:
             planner.dev_argmin_cost(db.cost, best)
 
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
+    ref_cost = db.cost.clone()
+    ref_assign_sum = int(db.assign.sum().item())
     planner.profile(True)
     if world > 1:
         dist.barrier()
@@ -129,6 +133,9 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    # every timed step re-planned the same inputs: its plans must be bit-identical
+    if not torch.equal(db.cost, ref_cost) or int(db.assign.sum().item()) != ref_assign_sum:
+        raise RuntimeError("timed steps did not reproduce the warmup plan (stream ordering bug?)")
     place_ms, place_n = planner.kernel_stats(FP_K_PLACE)
     sort_ms, sort_n = planner.kernel_stats(FP_K_SORT)
     best_id = int(best.item())

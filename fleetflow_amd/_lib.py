@@ -10,7 +10,9 @@ import ctypes as ct
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfleetplace.so")
+# FLEETPLACE_LIB selects another build of the same ABI (e.g. the diagnostics build
+# libfleetplace_stats.so used by tools/pipe_stats.py); default is the release build.
+LIB_PATH = os.environ.get("FLEETPLACE_LIB") or os.path.join(_HERE, "libfleetplace.so")
 
 FP_OK, FP_EINVAL, FP_ENOMEM, FP_EDEVICE, FP_EOVERFLOW, FP_ECORRUPT = 0, -1, -2, -3, -4, -5
 FP_NONE = 0xFFFFFFFF
@@ -59,6 +61,7 @@ SIGNATURES = {
     "fp_ctx_create": (ct.c_int, [ct.POINTER(vp), ct.c_int]),
     "fp_ctx_destroy": (None, [vp]),
     "fp_ctx_set_stream": (ct.c_int, [vp, vp]),
+    "fp_ctx_reset_stream": (ct.c_int, [vp]),
     "fp_ctx_sync": (ct.c_int, [vp]),
     "fp_strerror": (ct.c_char_p, [ct.c_int]),
     "fp_abi_version": (ct.c_int, []),

@@ -54,7 +54,7 @@ extern "C" int fp_ctx_create(fp_ctx **out, int device) {
 extern "C" void fp_ctx_destroy(fp_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream);
     for (auto &r : c->pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
     if (c->ws) (void)hipFree(c->ws);
@@ -67,7 +67,13 @@ extern "C" void fp_ctx_destroy(fp_ctx *c) {
 
 extern "C" int fp_ctx_set_stream(fp_ctx *c, void *s) {
     if (!c) return FP_EINVAL;
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->stream = (hipStream_t)s;  // NULL = HIP null stream
+    return FP_OK;
+}
+
+extern "C" int fp_ctx_reset_stream(fp_ctx *c) {
+    if (!c) return FP_EINVAL;
+    c->stream = c->own_stream;
     return FP_OK;
 }
 

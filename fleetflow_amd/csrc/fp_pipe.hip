@@ -1,37 +1,58 @@
 // fp_pipe.hip -- stage 3 FFD as an intra-workgroup tile pipeline (SPEC.md 2.3).
 //
-// One workgroup = one scenario.  Its N nodes are cut into W tiles of G x 64 nodes;
-// wave w owns tile w with the node state (cpu_free, mem_free, conflict_used,
-// labels) RESIDENT IN VGPRs (lane l of group g holds node w*G*64 + g*64 + l).
-// Containers stream through the waves in FFD order: wave 0 reads the sorted
-// container list from HBM, places what fits its tile (lowest node first) and
-// forwards the rest, in order, to wave 1 through an LDS ring, and so on; what
-// the last wave cannot place is NOFIT.
+// One workgroup = one scenario.  Its N nodes are cut into W tiles of G groups of
+// 64 nodes; wave w owns tile w.  Node records (cpu_free, mem_free,
+// conflict_used, labels) live in LDS as 16-byte AoS records, so a wave checks a
+// whole 64-node group with one ds_read_b128 per lane and a wavefront ballot
+// (lowest set lane = first fit inside the group).  Containers stream through the
+// waves in FFD order: wave 0 reads the sorted container list from HBM, places
+// what fits its tile and forwards the rest, in order, to wave 1 through an LDS
+// ring, and so on; what the last wave cannot place is NOFIT.
 //
 // Exactness: a container lands in the first tile holding a feasible node, and a
 // tile's state only depends on the containers that reached it, in FFD order --
 // so the pipeline computes exactly the sequential first fit.
 //
-// Pruning (exact): per tile, per 64-node group g and per threshold bucket k, two
-// 64-bit masks  B_cpu[g][k] = {l : sched && cpu_free >= Tc[k]} and
-// B_mem[g][k] = {l : sched && mem_free >= Tm[k]}  live in LDS.  A container with
-// bucket indices (kc, km) (Tc[kc] <= cpu, Tm[km] <= mem) can only fit nodes in
-// B_cpu[g][kc] & B_mem[g][km]; free capacity only shrinks (SPEC.md 2.3
-// monotonicity), so masks are maintained by clearing bits on placement and a
-// stale mask is always a superset.  Only candidate groups get the exact
-// register-resident check.
+// Pruning (exact): per 64-node group g and threshold bucket k, two 64-bit masks
+// B_cpu[g][k] = {l : sched && cpu_free >= Tc[k]} and B_mem[g][k] = {l : sched &&
+// mem_free >= Tm[k]}.  A container in buckets (kc, km) (Tc[kc] <= cpu,
+// Tm[km] <= mem) can only fit nodes in B_cpu[g][kc] & B_mem[g][km].  Free
+// capacity only shrinks (SPEC.md 2.3 monotonicity), so masks are maintained by
+// clearing bits on placement and a stale mask is always a superset: only
+// candidate groups get the exact check.
 #include "fp_internal.h"
+#include <stdlib.h>
+
+#ifdef FP_PIPE_STATS
+// diagnostics build only: per stage w: [0] visits [1] cand checks [2] hits [3] batches
+// [4] input-spin iterations [5] output-spin iterations, then s_memtime cycles in
+// [8] input [9] prescan [10] candidate loop [11] results+forward [12] output wait
+// [13] whole loop
+__device__ unsigned long long g_pipe_stats[16 * 16];
+#define STAT_ADD(w, i, v) atomicAdd(&g_pipe_stats[(w) * 16 + (i)], (unsigned long long)(v))
+#define STAT_CLK() __builtin_amdgcn_s_memtime()
+#define STAT_ON 1
+// per-batch timeline of scenario 0: [stage][batch] = (t_in_ready, t_prescan, t_cand, t_out_done)
+constexpr int TL_B = 2048;
+__device__ unsigned long long g_pipe_tl[16 * TL_B * 4];
+#else
+#define STAT_ADD(w, i, v) ((void)0)
+#define STAT_CLK() 0ull
+#define STAT_ON 0
+#endif
 
 namespace fpp {
 
 constexpr int K = 32;               // threshold buckets per dimension
-constexpr int R = 4;                // LDS ring slots per link
 constexpr uint32_t END = 0x80000000u;
 constexpr uint32_t CYC = 0x80000000u;
 constexpr uint32_t SPIN_LIMIT = 1u << 26;
+constexpr uint32_t MAX_G = 32;      // groups per stage (bit registers are u32)
+constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
+constexpr int SB = 8;               // containers per corner sub-batch
 
 struct PipeArgs {
-    uint32_t C, N, scen_base, W;
+    uint32_t C, N, scen_base, W, G, R;
     const uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;  // FFD-sorted SoA [S][C]; idx bit31 = CYCLE
     uint32_t *cf, *mf;
     const uint32_t *lab;
@@ -51,71 +72,14 @@ __device__ __forceinline__ void lds_rel(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int G>
-struct Tile {
-    uint32_t cf[G], mf[G], cu[G], lab[G];
-};
-
-// Exact check of group g (compile-time) for the wave-uniform container; on a hit
-// the winning lane's node is updated in registers and the LDS masks are cleared.
-template <int G, int g>
-__device__ __forceinline__ bool check_group(Tile<G> &t, uint64_t *Mg, uint64_t *Ug, uint32_t lane,
-                                            uint32_t c_cpu, uint32_t c_mem, uint32_t c_req, uint32_t c_conf,
-                                            uint32_t c_kc, uint32_t c_km, uint32_t my_tc, uint32_t my_tm,
-                                            uint32_t &n_used, uint32_t &node) {
-    const uint64_t wm = Mg[c_kc * 2] & Mg[c_km * 2 + 1];
-    const bool ok = fpd::fits(c_cpu, c_mem, c_req, c_conf, t.cf[g], t.mf[g], t.lab[g], t.cu[g]);
-    const uint64_t m = __ballot(ok) & wm;
-    if (!m) return false;
-    const uint32_t l = (uint32_t)__builtin_ctzll(m);
-    const uint32_t oc = __builtin_amdgcn_readlane(t.cf[g], l);
-    const uint32_t om = __builtin_amdgcn_readlane(t.mf[g], l);
-    const uint32_t nc = oc - c_cpu, nm = om - c_mem;
-    if (lane == l) {
-        t.cf[g] = nc;
-        t.mf[g] = nm;
-        t.cu[g] |= c_conf;
-    }
-    if (lane < (uint32_t)K) {
-        const uint64_t clr = ~(1ull << l);
-        if (my_tc <= oc && my_tc > nc) atomicAnd((unsigned long long *)&Mg[lane * 2], (unsigned long long)clr);
-        if (my_tm <= om && my_tm > nm) atomicAnd((unsigned long long *)&Mg[lane * 2 + 1], (unsigned long long)clr);
-    }
-    const uint64_t u = *Ug;
-    if (!((u >> l) & 1ull)) {
-        n_used++;
-        if (lane == 0) *Ug = u | (1ull << l);
-    }
-    node = (uint32_t)g * 64u + l;
-    return true;
-}
-
-// Balanced dispatch over candidate group gi in [LO, HI) to the compile-time check.
-template <int G, int LO, int HI>
-__device__ __forceinline__ bool dispatch(uint32_t gi, Tile<G> &t, uint64_t *M, uint64_t *U, uint32_t lane,
-                                         uint32_t c_cpu, uint32_t c_mem, uint32_t c_req, uint32_t c_conf,
-                                         uint32_t c_kc, uint32_t c_km, uint32_t my_tc, uint32_t my_tm,
-                                         uint32_t &n_used, uint32_t &node) {
-    if constexpr (HI - LO == 1) {
-        return check_group<G, LO>(t, M + (size_t)LO * K * 2, U + LO, lane, c_cpu, c_mem, c_req, c_conf, c_kc,
-                                  c_km, my_tc, my_tm, n_used, node);
-    } else {
-        constexpr int MID = (LO + HI) / 2;
-        if (gi < (uint32_t)MID)
-            return dispatch<G, LO, MID>(gi, t, M, U, lane, c_cpu, c_mem, c_req, c_conf, c_kc, c_km, my_tc, my_tm,
-                                        n_used, node);
-        return dispatch<G, MID, HI>(gi, t, M, U, lane, c_cpu, c_mem, c_req, c_conf, c_kc, c_km, my_tc, my_tm,
-                                    n_used, node);
-    }
-}
-
 // Spin on an LDS word until pred holds; bounded, with a workgroup abort flag.
 template <class Pred>
-__device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_flag, uint32_t *err) {
+__device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_flag, uint32_t *err,
+                                     uint32_t &iters) {
     uint32_t n = 0;
     while (true) {
         const uint32_t v = lds_acq(word);
-        if (pred(v)) return true;
+        if (pred(v)) { iters += n; return true; }
         if (lds_acq(abort_flag)) return false;
         if (++n > SPIN_LIMIT) {
             lds_rel(abort_flag, 1u);
@@ -126,72 +90,92 @@ __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_
     }
 }
 
-// LDS layout (bytes, all offsets 16-aligned):
-//   M   : W*G*K*2 u64   (B_cpu, B_mem interleaved per (g, k))
-//   U   : W*G u64       (node-used masks)
-//   CTL : (W-1)*8 u32   per link: [0]=head [1]=tail [2..2+R)=slot counts
-//   CNT : 8 u32         [0]=n_used [1]=n_rej [2]=abort
-//   D   : (W-1)*R*6*64 u32 ring data (cpu, mem, req, conf, idx, kk) per slot
-template <int G, int MAXW>
-__global__ __launch_bounds__(MAXW * 64) void k_ffd_pipe(const PipeArgs a) {
+// lane `t` of `old` replaced by the wave-uniform `val` (v_cmp + v_cndmask)
+#define WRITELANE(val, t, old) ((lane == (t)) ? (uint32_t)(val) : (old))
+
+// bucket index: largest k with T[k] <= v (T ascending, T[0] = 0; lane base + k holds
+// T[k]).  Binary search through ds_bpermute: no scalar registers held across the
+// main loop (hoisted per-threshold readlanes spill SGPRs).
+__device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t my_t, int base) {
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t step = K / 2; step; step >>= 1) {
+        const uint32_t t = (uint32_t)__shfl((int)my_t, (int)(base + k + step));
+        k += t <= v ? step : 0u;
+    }
+    return k;
+}
+
+// LDS layout (bytes; every region 16-aligned):
+//   REC : W*G*64 uint4          node records (cf, mf, cu, lab) of every tile
+//   M   : W*G*K*2 u64           B_cpu / B_mem interleaved per (g, k)
+//   CTL : (W-1)*8 u32 + 8 u32   per link [0]=head [1]=tail [2..2+R)=slot counts; then
+//                               CNT [0]=n_used [1]=n_rej [2]=abort
+//   D   : (W-1)*R*NF*64 u32     ring slots, field-major
+__global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t W = a.W;
+    const uint32_t W = a.W, G = a.G, R = a.R;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t s = blockIdx.x;
     const uint32_t C = a.C, N = a.N;
     const size_t cb = (size_t)s * C, nb = (size_t)s * N;
 
-    uint64_t *M = reinterpret_cast<uint64_t *>(smem);
-    uint64_t *U = M + (size_t)W * G * K * 2;
-    uint32_t *CTL = reinterpret_cast<uint32_t *>(U + (size_t)W * G);
+    uint4 *REC = reinterpret_cast<uint4 *>(smem);
+    uint64_t *M = reinterpret_cast<uint64_t *>(REC + (size_t)W * G * 64);
+    uint32_t *CTL = reinterpret_cast<uint32_t *>(M + (size_t)W * G * K * 2);
     uint32_t *CNT = CTL + (W - 1) * 8;
     uint32_t *D = CNT + 8;
 
     for (uint32_t i = threadIdx.x; i < (W - 1) * 8 + 8; i += blockDim.x) CTL[i] = 0;
 
-    // ---- load the tile into VGPRs and build the bucket masks ----
-    const uint32_t my_tc = lane < (uint32_t)K ? a.tc[lane] : 0xFFFFFFFFu;
-    const uint32_t my_tm = lane < (uint32_t)K ? a.tm[lane] : 0xFFFFFFFFu;
-    const uint32_t nbase = w * G * 64;
-    Tile<G> t;
-    uint64_t *Mw = M + (size_t)w * G * K * 2;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint32_t n = nbase + g * 64 + lane;
+    // ---- stage the tile into LDS and build the bucket masks ----
+    // lane k < 32 holds Tc[k], lane 32 + k holds Tm[k] (K == 32: one wave covers both)
+    static_assert(K == 32, "mask/threshold lane layout assumes K == 32");
+    const uint32_t my_t = lane < (uint32_t)K ? a.tc[lane] : a.tm[lane - K];
+    const uint32_t gbase = w * G;                       // first group of this tile
+    uint4 *Rw = REC + (size_t)gbase * 64;
+    uint64_t *Mw = M + (size_t)gbase * K * 2;
+    uint32_t schedbits = 0, usedbits = 0;               // bit g for node (g, lane)
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t n = (gbase + g) * 64 + lane;
         const bool in = n < N;
         const bool sc = in && a.sched[nb + n] != 0;
-        t.cf[g] = in ? a.cf[nb + n] : 0u;
-        t.mf[g] = in ? a.mf[nb + n] : 0u;
-        t.cu[g] = in ? a.cu[nb + n] : 0u;
-        t.lab[g] = in ? a.lab[nb + n] : 0u;
-#pragma unroll 1
-        for (int k = 0; k < K; ++k) {
-            const uint32_t tck = __builtin_amdgcn_readlane(my_tc, k);
-            const uint32_t tmk = __builtin_amdgcn_readlane(my_tm, k);
-            const uint64_t bc = __ballot(sc && t.cf[g] >= tck);
-            const uint64_t bm = __ballot(sc && t.mf[g] >= tmk);
-            if (lane == 0) {
+        uint4 r;
+        r.x = in ? a.cf[nb + n] : 0u;
+        r.y = in ? a.mf[nb + n] : 0u;
+        r.z = in ? a.cu[nb + n] : 0u;
+        r.w = in ? a.lab[nb + n] : 0u;
+        Rw[g * 64 + lane] = r;
+        schedbits |= sc ? (1u << g) : 0u;
+        for (int k = 0; k < K; ++k) {  // every lane takes part in each ballot
+            const uint64_t bc = __builtin_amdgcn_ballot_w64(sc & (r.x >= __builtin_amdgcn_readlane(my_t, k)));
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(sc & (r.y >= __builtin_amdgcn_readlane(my_t, K + k)));
+            if (lane == (uint32_t)k) {
                 Mw[((size_t)g * K + k) * 2] = bc;
                 Mw[((size_t)g * K + k) * 2 + 1] = bm;
             }
         }
-        if (lane == 0) U[(size_t)w * G + g] = 0;
     }
     __syncthreads();
 
     const bool has_out = w + 1 < W;
     uint32_t *octl = CTL + w * 8;
     uint32_t *ictl = CTL + (w - 1) * 8;
-    uint32_t *odata = D + (size_t)w * R * 6 * 64;
-    uint32_t *idata = D + (size_t)(w - 1) * R * 6 * 64;
+    uint32_t *odata = D + (size_t)w * R * NF * 64;
+    uint32_t *idata = D + (size_t)(w - 1) * R * NF * 64;
     uint32_t *abort_flag = &CNT[2];
     uint32_t ohead = 0, ofill = 0, itail = 0, k0 = 0;
     uint32_t n_used = 0, n_rej = 0;
+    uint32_t st_spin_in = 0, st_spin_out = 0, st_visits = 0, st_checks = 0, st_hits = 0, st_batches = 0;
+    unsigned long long ck_in = 0, ck_pre = 0, ck_cand = 0, ck_fwd = 0, ck_wait = 0;
+    const unsigned long long ck_t0 = STAT_CLK();
+    unsigned long long ck_a, ck_b;
     bool alive = true;
 
     while (alive) {
-        uint32_t cpu = 0, mem = 0, req = 0, conf = 0, idx = 0, kk = 0;
+        ck_a = STAT_CLK();
+        uint32_t cpu = 0, mem = 0, req = 0, conf = 0, idx = 0;
         bool valid = false;
         if (w == 0) {
             if (k0 >= C) break;
@@ -212,20 +196,14 @@ __global__ __launch_bounds__(MAXW * 64) void k_ffd_pipe(const PipeArgs a) {
             }
             n_rej += (uint32_t)__popcll(__ballot(cyc));
             valid = valid && !cyc;
-            uint32_t kc = 0, km = 0;
-            for (int k = 1; k < K; ++k) {
-                kc += cpu >= __builtin_amdgcn_readlane(my_tc, k) ? 1u : 0u;
-                km += mem >= __builtin_amdgcn_readlane(my_tm, k) ? 1u : 0u;
-            }
-            kk = kc | (km << 8);
             k0 += 64;
         } else {
             const uint32_t want = itail;
-            if (!spin(&ictl[0], [want](uint32_t h) { return h != want; }, abort_flag, a.err)) break;
+            if (!spin(&ictl[0], [want](uint32_t h) { return h != want; }, abort_flag, a.err, st_spin_in)) break;
             const uint32_t slot = itail % R;
             const uint32_t n = ictl[2 + slot];
             if (n & END) break;
-            const uint32_t *sd = idata + (size_t)slot * 6 * 64;
+            const uint32_t *sd = idata + (size_t)slot * NF * 64;
             valid = lane < n;
             if (valid) {
                 cpu = sd[lane];
@@ -233,51 +211,132 @@ __global__ __launch_bounds__(MAXW * 64) void k_ffd_pipe(const PipeArgs a) {
                 req = sd[128 + lane];
                 conf = sd[192 + lane];
                 idx = sd[256 + lane];
-                kk = sd[320 + lane];
             }
             itail++;
             lds_rel(&ictl[1], itail);
         }
-        const uint32_t kc = kk & 0xFFu, km = kk >> 8;
+        const uint32_t kc = bucket_of(cpu, my_t, 0), km = bucket_of(mem, my_t, K);
+        ck_b = STAT_CLK(); ck_in += ck_b - ck_a; ck_a = ck_b;
+#ifdef FP_PIPE_STATS
+        const unsigned long long ck_t0_batch = ck_b;
+#endif
 
-        // lane-parallel candidate groups (superset; masks only lose bits)
-        uint32_t cand = 0;
-        if (valid) {
-#pragma unroll 4
-            for (int g = 0; g < G; ++g) {
-                const uint64_t *mg = Mw + (size_t)g * K * 2;
-                if (mg[kc * 2] & mg[km * 2 + 1]) cand |= 1u << g;
-            }
+        // Lane-parallel candidate groups, a superset of the feasible groups (masks
+        // only lose bits).  Two filters are ANDed:
+        //  * per-container bucket masks B_cpu[g][kc] & B_mem[g][km];
+        //  * an exact 2-D "corner" mask per sub-batch q of SB consecutive containers:
+        //    E_q[g] = {l : sched && cpu_free >= min cpu(q) && mem_free >= min mem(q)}.
+        //    FFD order makes sub-batches homogeneous, so the corner is tight.
+        const uint32_t vc = valid ? cpu : 0xFFFFFFFFu, vm = valid ? mem : 0xFFFFFFFFu;
+        uint32_t qc = vc, qm = vm;  // min over the lane's sub-batch (xor butterfly)
+#pragma unroll
+        for (int o = 1; o < SB; o <<= 1) {
+            qc = min(qc, (uint32_t)__shfl_xor((int)qc, o));
+            qm = min(qm, (uint32_t)__shfl_xor((int)qm, o));
         }
-        uint64_t todo = __ballot(cand != 0);
+        uint32_t cand = 0;
+        const uint32_t my_q = lane / SB;
+        // the 64/SB corners, broadcast into VGPRs (readlane-to-SGPR copies of them get
+        // hoisted out of the loops and spill scalar registers)
+        uint32_t cqv[64 / SB], mqv[64 / SB];
+#pragma unroll
+        for (uint32_t q = 0; q < 64 / SB; ++q) {
+            cqv[q] = (uint32_t)__shfl((int)qc, (int)(q * SB));
+            mqv[q] = (uint32_t)__shfl((int)qm, (int)(q * SB));
+        }
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint4 r = Rw[g * 64 + lane];
+            const bool sc = (schedbits >> g) & 1u;
+            uint64_t e = 0;  // E_{my_q}[g]
+#pragma unroll
+            for (uint32_t q = 0; q < 64 / SB; ++q) {
+                const uint64_t eq = __builtin_amdgcn_ballot_w64(sc & (r.x >= cqv[q]) & (r.y >= mqv[q]));
+                e = my_q == q ? eq : e;
+            }
+            const uint64_t *mg = Mw + (size_t)g * K * 2;
+            if (valid && (mg[kc * 2] & mg[km * 2 + 1] & e)) cand |= 1u << g;
+        }
+        uint64_t todo = __builtin_amdgcn_ballot_w64(cand != 0);
         uint64_t placed = 0;
         uint32_t my_assign = FP_NONE;
-        while (todo) {
-            const uint32_t ti = (uint32_t)__builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint32_t c_cpu = __builtin_amdgcn_readlane(cpu, ti);
-            const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
-            const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
-            const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
-            const uint32_t c_kk = __builtin_amdgcn_readlane(kk, ti);
-            uint32_t cc = __builtin_amdgcn_readlane(cand, ti);
-            const uint32_t c_kc = c_kk & 0xFFu, c_km = c_kk >> 8;
-            while (cc) {
-                const uint32_t gi = (uint32_t)__builtin_ctz(cc);
-                cc &= cc - 1;
-                uint32_t node = 0;
-                if (dispatch<G, 0, G>(gi, t, Mw, U + (size_t)w * G, lane, c_cpu, c_mem, c_req, c_conf, c_kc, c_km,
-                                      my_tc, my_tm, n_used, node)) {
-                    placed |= 1ull << ti;
-                    if (lane == ti) my_assign = nbase + node;
-                    break;
+        if (STAT_ON) {
+            st_batches++;
+            st_visits += (uint32_t)__popcll(__ballot(valid));
+        }
+        ck_b = STAT_CLK(); ck_pre += ck_b - ck_a; ck_a = ck_b;
+#ifdef FP_PIPE_STATS
+        const unsigned long long tl_pre = ck_b;
+#endif
+        // Exact first fit, container by container in FFD order.  The records of the
+        // last group touched stay in registers (g_reg, r_reg): consecutive containers
+        // mostly hit the same "frontier" group, so a placement there is a register
+        // update plus a fire-and-forget LDS write, with no LDS read to wait for.  LDS
+        // is re-read only when the candidate group changes (all writes go through
+        // r_reg first, so register and LDS copies never disagree).
+        {
+            uint32_t g_reg = 0xFFFFFFFFu;
+            uint4 r_reg = make_uint4(0u, 0u, 0u, 0u);
+            while (todo) {
+                const uint32_t ti = (uint32_t)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                const uint32_t c_cpu = __builtin_amdgcn_readlane(cpu, ti);
+                const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
+                const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
+                const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
+                uint32_t cc = __builtin_amdgcn_readlane(cand, ti);
+                while (cc) {
+                    const uint32_t g = (uint32_t)__builtin_ctz(cc);
+                    cc &= cc - 1;
+                    if (g != g_reg) {
+                        r_reg = Rw[g * 64 + lane];
+                        g_reg = g;
+                    }
+                    if (STAT_ON) st_checks++;
+                    const bool ok = ((schedbits >> g) & 1u) & (r_reg.x >= c_cpu) & (r_reg.y >= c_mem) &
+                                    ((r_reg.w & c_req) == c_req) & ((r_reg.z & c_conf) == 0u);
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+                    if (m) {
+                        // placement, branch-free: lane l's record changes; one all-lane
+                        // ds_and_b64 clears the crossed buckets (lanes 0-31 cpu masks,
+                        // lanes 32-63 mem masks of group g)
+                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                        const uint32_t oc = __builtin_amdgcn_readlane(r_reg.x, l);
+                        const uint32_t om = __builtin_amdgcn_readlane(r_reg.y, l);
+                        const uint32_t nc = oc - c_cpu, nm = om - c_mem;
+                        const bool me = lane == l;
+                        r_reg.x = me ? nc : r_reg.x;
+                        r_reg.y = me ? nm : r_reg.y;
+                        r_reg.z = me ? (r_reg.z | c_conf) : r_reg.z;
+                        Rw[g * 64 + lane] = r_reg;
+                        const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
+                        const bool crossed = (my_t <= ov) & (my_t > nv);
+                        atomicAnd((unsigned long long *)&Mw[(size_t)g * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
+                                  crossed ? ~(1ull << l) : ~0ull);
+                        n_used += ((__builtin_amdgcn_readlane(usedbits, l) >> g) & 1u) ^ 1u;
+                        usedbits |= me ? (1u << g) : 0u;
+                        placed |= 1ull << ti;
+                        my_assign = WRITELANE((gbase + g) * 64 + l, ti, my_assign);
+                        if (STAT_ON) st_hits++;
+                        break;
+                    }
                 }
             }
         }
+        ck_b = STAT_CLK(); ck_cand += ck_b - ck_a; ck_a = ck_b;
+#ifdef FP_PIPE_STATS
+        const unsigned long long tl_cand = ck_b;
+        const uint32_t tl_idx = st_batches - 1;
+#endif
         if ((placed >> lane) & 1ull) {
             a.assign[cb + idx] = my_assign;
             a.reason[cb + idx] = FP_REASON_OK;
         }
+#ifdef FP_PIPE_STATS
+        if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B) {
+            unsigned long long *tl = &g_pipe_tl[((size_t)w * TL_B + tl_idx) * 4];
+            tl[0] = ck_t0_batch; tl[1] = tl_pre; tl[2] = tl_cand;
+        }
+#endif
         const bool fwd = valid && !((placed >> lane) & 1ull);
         if (!has_out) {
             if (fwd) {
@@ -291,25 +350,25 @@ __global__ __launch_bounds__(MAXW * 64) void k_ffd_pipe(const PipeArgs a) {
         const uint32_t f = (uint32_t)__popcll(fm);
         if (!f) continue;
         const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-        uint32_t *od = odata + (size_t)(ohead % R) * 6 * 64;
+        uint32_t *od = odata + (size_t)(ohead % R) * NF * 64;
         if (fwd && pos < 64) {
-            od[pos] = cpu; od[64 + pos] = mem; od[128 + pos] = req;
-            od[192 + pos] = conf; od[256 + pos] = idx; od[320 + pos] = kk;
+            od[pos] = cpu; od[64 + pos] = mem; od[128 + pos] = req; od[192 + pos] = conf; od[256 + pos] = idx;
         }
         if (ofill + f >= 64) {
             octl[2 + ohead % R] = 64;
             ohead++;
             lds_rel(&octl[0], ohead);
             const uint32_t h = ohead;
-            if (!spin(&octl[1], [h](uint32_t tl) { return h - tl < (uint32_t)R; }, abort_flag, a.err)) {
+            ck_b = STAT_CLK(); ck_fwd += ck_b - ck_a; ck_a = ck_b;
+            if (!spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, st_spin_out)) {
                 alive = false;
                 break;
             }
-            od = odata + (size_t)(ohead % R) * 6 * 64;
+            ck_b = STAT_CLK(); ck_wait += ck_b - ck_a; ck_a = ck_b;
+            od = odata + (size_t)(ohead % R) * NF * 64;
             if (fwd && pos >= 64) {
                 const uint32_t p = pos - 64;
-                od[p] = cpu; od[64 + p] = mem; od[128 + p] = req;
-                od[192 + p] = conf; od[256 + p] = idx; od[320 + p] = kk;
+                od[p] = cpu; od[64 + p] = mem; od[128 + p] = req; od[192 + p] = conf; od[256 + p] = idx;
             }
             ofill = ofill + f - 64;
         } else {
@@ -325,7 +384,7 @@ __global__ __launch_bounds__(MAXW * 64) void k_ffd_pipe(const PipeArgs a) {
             ohead++;
             lds_rel(&octl[0], ohead);
             const uint32_t h = ohead;
-            ok = spin(&octl[1], [h](uint32_t tl) { return h - tl < (uint32_t)R; }, abort_flag, a.err);
+            ok = spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, st_spin_out);
         }
         if (ok) {
             octl[2 + ohead % R] = END;
@@ -336,14 +395,21 @@ __global__ __launch_bounds__(MAXW * 64) void k_ffd_pipe(const PipeArgs a) {
     if (lane == 0) {
         atomicAdd(&CNT[0], n_used);
         atomicAdd(&CNT[1], n_rej);
+        STAT_ADD(w, 0, st_visits); STAT_ADD(w, 1, st_checks); STAT_ADD(w, 2, st_hits);
+        STAT_ADD(w, 3, st_batches); STAT_ADD(w, 4, st_spin_in); STAT_ADD(w, 5, st_spin_out);
+        STAT_ADD(w, 8, ck_in); STAT_ADD(w, 9, ck_pre); STAT_ADD(w, 10, ck_cand); STAT_ADD(w, 11, ck_fwd);
+        STAT_ADD(w, 12, ck_wait); STAT_ADD(w, 13, STAT_CLK() - ck_t0);
     }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint32_t n = nbase + g * 64 + lane;
+    (void)ck_t0; (void)ck_in; (void)ck_pre; (void)ck_cand; (void)ck_fwd; (void)ck_wait;
+    (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
+    // write the tile's node state back (LDS -> HBM)
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t n = (gbase + g) * 64 + lane;
         if (n < N) {
-            a.cf[nb + n] = t.cf[g];
-            a.mf[nb + n] = t.mf[g];
-            a.cu[nb + n] = t.cu[g];
+            const uint4 r = Rw[g * 64 + lane];
+            a.cf[nb + n] = r.x;
+            a.mf[nb + n] = r.y;
+            a.cu[nb + n] = r.z;
         }
     }
     __syncthreads();
@@ -370,47 +436,66 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
     }
 }
 
-size_t lds_bytes(uint32_t W, uint32_t G) {
-    return (size_t)W * G * K * 16 + (size_t)W * G * 8 + ((size_t)(W - 1) * 8 + 8) * 4 +
-           (size_t)(W - 1) * R * 6 * 64 * 4;
+size_t lds_bytes(uint32_t W, uint32_t G, uint32_t R) {
+    return (size_t)W * G * 64 * 16 + (size_t)W * G * K * 16 + ((size_t)(W - 1) * 8 + 8) * 4 +
+           (size_t)(W - 1) * R * NF * 64 * 4;
 }
 
 }  // namespace fpp
 
 using namespace fpp;
 
-static const int kGs[] = {2, 4, 8, 12, 16, 20, 24, 32};
+static void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
+    T[0] = 0;
+    if (lo == 0) lo = 1;
+    if (hi < lo) hi = lo;
+    const double r = pow((double)hi / (double)lo, 1.0 / (double)(K - 2));
+    double v = (double)lo;
+    for (int k = 1; k < K; ++k) {
+        uint32_t x = k == K - 1 ? hi : (uint32_t)ceil(v);
+        if (x < T[k - 1]) x = T[k - 1];
+        if (x > hi) x = hi;
+        T[k] = x;
+        v *= r;
+    }
+}
 
-// Largest workgroup (in waves) instantiated for a tile of G groups: VGPR budget
-// is 512 / (waves per SIMD), and the tile alone takes 4*G VGPRs.
-static inline uint32_t max_waves_for(int G) { return G <= 4 ? 16u : (G <= 24 ? 8u : 4u); }
-
-// Picks (G, W) for NG groups; returns false when the tile pipeline cannot host N.
+// Picks (G, W) for N nodes: prefer 8 stages (two waves per SIMD), then fewer or
+// more; false when one CU's LDS cannot hold the scenario.
 bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, size_t *lds_out) {
     const uint32_t NG = (N + 63) / 64;
+    const size_t cap = 160 * 1024;
     if (NG == 0) {
-        *G_out = 2; *W_out = 1; *lds_out = lds_bytes(1, 2);
+        *G_out = 1; *W_out = 1; *lds_out = lds_bytes(1, 1, 2);
         return true;
     }
-    for (uint32_t wmax : {4u, 8u, 16u}) {
-        for (int G : kGs) {
-            const uint32_t W = (NG + G - 1) / G;
-            if (W > wmax || W > max_waves_for(G)) continue;
-            const size_t lds = lds_bytes(W, G);
-            if (lds > 160 * 1024) continue;
-            *G_out = G; *W_out = W; *lds_out = lds;
-            return true;
-        }
+    // FLEETPLACE_PIPE_W: force the stage count (tuning experiments only)
+    static const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
+    for (uint32_t W : {8u, 4u, 2u, 1u, 12u, 16u}) {
+        if (forced_w > 0 && W != (uint32_t)forced_w) continue;
+        if (W > NG && W > 1) continue;
+        const uint32_t G = (NG + W - 1) / W;
+        if (G > MAX_G) continue;
+        const uint32_t Wn = (NG + G - 1) / G;  // drop empty tail stages
+        const size_t lds = lds_bytes(Wn, G, 2);
+        if (lds > cap) continue;
+        *G_out = G; *W_out = Wn; *lds_out = lds;
+        return true;
     }
     return false;
 }
 
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
-                   const fp_batch *b, uint32_t maxc, uint32_t maxm) {
+                   const fp_batch *b, uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
     uint32_t G, W;
     size_t lds;
     if (!fp_pipe_plan(N, &G, &W, &lds)) return FP_EOVERFLOW;
     if (C >= 0x80000000u) return FP_EOVERFLOW;
+    // deepest ring (2..4 slots) that still fits the CU's LDS
+    uint32_t R = 2;
+    for (uint32_t r = 4; r > 2; --r)
+        if (lds_bytes(W, G, r) <= 160 * 1024) { R = r; break; }
+    lds = lds_bytes(W, G, R);
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;
     uint32_t *s_cpu = (uint32_t *)fp_ws_take(c, SC * 4);
@@ -427,40 +512,37 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         FP_HIP(hipGetLastError());
     }
     PipeArgs a;
-    a.C = C; a.N = N; a.scen_base = scen_base; a.W = W;
+    a.C = C; a.N = N; a.scen_base = scen_base; a.W = W; a.G = G; a.R = R;
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
     a.assign = b->assign; a.reason = b->reason; a.cost = b->cost; a.err = c->d_err;
-    // thresholds: T0 = 0, then quarter-octave steps up to the batch maximum
-    a.tc[0] = 0; a.tm[0] = 0;
-    for (int k = 1; k < K; ++k) {
-        const double e = -(double)(K - 1 - k) / 4.0;
-        uint32_t vc = (uint32_t)ceil((double)maxc * pow(2.0, e));
-        uint32_t vm = (uint32_t)ceil((double)maxm * pow(2.0, e));
-        a.tc[k] = vc > a.tc[k - 1] ? vc : a.tc[k - 1];
-        a.tm[k] = vm > a.tm[k - 1] ? vm : a.tm[k - 1];
-    }
-    // instantiation: smallest MAXW bucket (4, 8, 16) that holds W waves
-    const uint32_t MW = W <= 4 ? 4 : (W <= 8 ? 8 : 16);
-    const void *fn = nullptr;
-#define FP_PIPE_CASE(GG, MM) \
-    if (G == GG && MW == MM) fn = (const void *)k_ffd_pipe<GG, MM>;
-    FP_PIPE_CASE(2, 4) FP_PIPE_CASE(2, 8) FP_PIPE_CASE(2, 16)
-    FP_PIPE_CASE(4, 4) FP_PIPE_CASE(4, 8) FP_PIPE_CASE(4, 16)
-    FP_PIPE_CASE(8, 4) FP_PIPE_CASE(8, 8)
-    FP_PIPE_CASE(12, 4) FP_PIPE_CASE(12, 8)
-    FP_PIPE_CASE(16, 4) FP_PIPE_CASE(16, 8)
-    FP_PIPE_CASE(20, 4) FP_PIPE_CASE(20, 8)
-    FP_PIPE_CASE(24, 4) FP_PIPE_CASE(24, 8)
-    FP_PIPE_CASE(32, 4)
-#undef FP_PIPE_CASE
-    if (!fn) return FP_EINVAL;
-    FP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // thresholds: T0 = 0, then K-1 geometric steps from the smallest positive to
+    // the largest demand of the batch (any ascending choice is exact; this one
+    // only decides how tight the candidate masks are)
+    fp_thresholds(minc, maxc, a.tc);
+    fp_thresholds(minm, maxm, a.tm);
+    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
-    void *kargs[] = {(void *)&a};
-    FP_HIP(hipLaunchKernel(fn, dim3(S), dim3(W * 64), kargs, lds, st));
+    k_ffd_pipe<<<S, W * 64, lds, st>>>(a);
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
     return FP_OK;
 }
+
+#ifdef FP_PIPE_STATS
+extern "C" int fp_debug_pipe_timeline(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_tl), sizeof(unsigned long long) * 16 * TL_B * 4) != hipSuccess)
+        return FP_EDEVICE;
+    return FP_OK;
+}
+extern "C" int fp_debug_pipe_stats(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_stats), sizeof(unsigned long long) * 16 * 16) != hipSuccess)
+        return FP_EDEVICE;
+    if (reset) {
+        static unsigned long long zero[16 * 16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pipe_stats), zero, sizeof(zero)) != hipSuccess) return FP_EDEVICE;
+    }
+    return FP_OK;
+}
+#endif

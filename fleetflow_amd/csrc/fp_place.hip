@@ -15,21 +15,29 @@ namespace {
 
 constexpr int kWave = 64;
 
+// out[0..1] = max(cpu), max(mem); out[2..3] = min positive cpu, mem (0xFFFFFFFF if none)
 __global__ void k_key_bounds(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
-                             size_t n, uint32_t *__restrict__ out /* [2] */) {
-    uint32_t mc = 0, mm = 0;
+                             size_t n, uint32_t *__restrict__ out /* [4] */) {
+    uint32_t mc = 0, mm = 0, lc = 0xFFFFFFFFu, lm = 0xFFFFFFFFu;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
-        mc = max(mc, cpu[i]);
-        mm = max(mm, mem[i]);
+        const uint32_t c = cpu[i], m = mem[i];
+        mc = max(mc, c);
+        mm = max(mm, m);
+        if (c) lc = min(lc, c);
+        if (m) lm = min(lm, m);
     }
     for (int o = 32; o > 0; o >>= 1) {
         mc = max(mc, (uint32_t)__shfl_xor((int)mc, o));
         mm = max(mm, (uint32_t)__shfl_xor((int)mm, o));
+        lc = min(lc, (uint32_t)__shfl_xor((int)lc, o));
+        lm = min(lm, (uint32_t)__shfl_xor((int)lm, o));
     }
     if ((threadIdx.x & 63) == 0) {
         atomicMax(&out[0], mc);
         atomicMax(&out[1], mm);
+        atomicMin(&out[2], lc);
+        atomicMin(&out[3], lm);
     }
 }
 
@@ -263,12 +271,14 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_SORT, &ev);
     FP_HIP(hipMemsetAsync(bounds, 0, 8, st));
+    FP_HIP(hipMemsetAsync(bounds + 2, 0xFF, 8, st));
     k_key_bounds<<<grid_for(SC, 256) < 1024 ? grid_for(SC, 256) : 1024, 256, 0, st>>>(
         b->cpu_m, b->mem_mib, SC, bounds);
     FP_HIP(hipGetLastError());
-    FP_HIP(hipMemcpyAsync(c->h_small, bounds, 8, hipMemcpyDeviceToHost, st));
+    FP_HIP(hipMemcpyAsync(c->h_small, bounds, 16, hipMemcpyDeviceToHost, st));
     FP_HIP(hipStreamSynchronize(st));
     const uint32_t maxc = ((uint32_t *)c->h_small)[0], maxm = ((uint32_t *)c->h_small)[1];
+    const uint32_t minc = ((uint32_t *)c->h_small)[2], minm = ((uint32_t *)c->h_small)[3];
     const uint32_t cbits = fp_bitwidth(maxc), mbits = fp_bitwidth(maxm);
     const uint32_t kbits = cbits + mbits;
     const uint64_t cmax = cbits ? ((cbits == 64 ? ~0ull : ((1ull << cbits) - 1))) : 0ull;
@@ -295,7 +305,8 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     uint32_t pG, pW;
     size_t plds;
     if (fp_pipe_plan(N, &pG, &pW, &plds))
-        return fp_pipe_launch(c, S, C, N, b->scen_base, order, b, maxc, maxm);
+        return fp_pipe_launch(c, S, C, N, b->scen_base, order, b, minc == 0xFFFFFFFFu ? 1u : minc, maxc,
+                              minm == 0xFFFFFFFFu ? 1u : minm, maxm);
     FfdArgs a;
     a.S = S; a.C = C; a.N = N; a.scen_base = b->scen_base;
     a.cpu = b->cpu_m; a.mem = b->mem_mib; a.req = b->req_labels; a.conf = b->conflict;

@@ -56,8 +56,12 @@ class Planner:
     def __exit__(self, *exc):
         self.close()
 
-    def set_stream(self, hip_stream_handle: int | None):
-        check(self._L.fp_ctx_set_stream(self._ctx, hip_stream_handle or None), "fp_ctx_set_stream")
+    def set_stream(self, hip_stream_handle: int):
+        """Launch on this hipStream_t handle; 0 is the HIP null (default) stream."""
+        check(self._L.fp_ctx_set_stream(self._ctx, ct.c_void_p(int(hip_stream_handle))), "fp_ctx_set_stream")
+
+    def reset_stream(self):
+        check(self._L.fp_ctx_reset_stream(self._ctx), "fp_ctx_reset_stream")
 
     def sync(self):
         check(self._L.fp_ctx_sync(self._ctx), "fp_ctx_sync")

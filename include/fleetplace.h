@@ -98,9 +98,11 @@ typedef struct {
 /* ---- context ------------------------------------------------------------ */
 int fp_ctx_create(fp_ctx **out, int device);
 void fp_ctx_destroy(fp_ctx *ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+/* Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream).
+ * NULL selects the HIP null (default) stream; fp_ctx_reset_stream restores the
+ * context's own non-blocking stream. */
 int fp_ctx_set_stream(fp_ctx *ctx, void *hip_stream);
+int fp_ctx_reset_stream(fp_ctx *ctx);
 int fp_ctx_sync(fp_ctx *ctx);
 const char *fp_strerror(int code);
 int fp_abi_version(void);
