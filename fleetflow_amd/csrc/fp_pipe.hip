@@ -46,13 +46,23 @@ namespace fpp {
 constexpr int K = 32;               // threshold buckets per dimension
 constexpr uint32_t END = 0x80000000u;
 constexpr uint32_t CYC = 0x80000000u;
-constexpr uint32_t SPIN_LIMIT = 1u << 26;
+// Deadlock guard: a wait longer than this (s_memrealtime runs at 100 MHz) aborts the
+// launch with FP_EDEVICE.  Downstream stages legitimately wait for most of a long
+// launch, so the bound is wall-clock time, not an iteration count.
+constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s
 constexpr uint32_t MAX_G = 32;      // groups per stage (bit registers are u32)
 constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
 constexpr int SB = 8;               // containers per corner sub-batch
 
 struct PipeArgs {
     uint32_t C, N, scen_base, W, G, R;
+    uint32_t B;       // segments (workgroups) per scenario
+    uint32_t slots;   // slots per global link (every container fits: never blocks)
+    uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
+    uint32_t *gabort; // launch-wide abort word (bounded spins)
+    uint32_t *ghead;  // [S][B-1] link heads, 128 B apart
+    uint32_t *gdata;  // [S][B-1][slots][6][64] link slots: row 0 = count, rows 1..5 = fields
+    uint32_t *part;   // [S][B][2] per-segment (n_used, n_rej)
     const uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;  // FFD-sorted SoA [S][C]; idx bit31 = CYCLE
     uint32_t *cf, *mf;
     const uint32_t *lab;
@@ -72,19 +82,37 @@ __device__ __forceinline__ void lds_rel(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Cross-workgroup links follow MI355X_MICROARCH.md "Valid forms", table row 1:
+// every payload dword is stored sc1 (relaxed agent-scope store), the storing wave
+// drains with s_waitcnt vmcnt(0), then ONE lane stores the head with an agent-scope
+// atomic store; the consumer polls the head with sc1 loads and reads every payload
+// dword with sc1 loads, so no acquire fence is needed.
+__device__ __forceinline__ uint32_t g_ld(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_st(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Spin on an LDS word until pred holds; bounded, with a workgroup abort flag.
 template <class Pred>
 __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_flag, uint32_t *err,
                                      uint32_t &iters) {
     uint32_t n = 0;
+    uint64_t t0 = 0;
     while (true) {
         const uint32_t v = lds_acq(word);
         if (pred(v)) { iters += n; return true; }
         if (lds_acq(abort_flag)) return false;
-        if (++n > SPIN_LIMIT) {
-            lds_rel(abort_flag, 1u);
-            if ((threadIdx.x & 63) == 0) atomicMax(err, (uint32_t)(-FP_EDEVICE));
-            return false;
+        if ((++n & 1023u) == 0) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (!t0) {
+                t0 = now;
+            } else if (now - t0 > SPIN_TICKS) {
+                lds_rel(abort_flag, 1u);
+                if ((threadIdx.x & 63) == 0) atomicMax(err, (uint32_t)(-FP_EDEVICE));
+                return false;
+            }
         }
         __builtin_amdgcn_s_sleep(1);
     }
@@ -114,12 +142,10 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t my_t, int bas
 //   D   : (W-1)*R*NF*64 u32     ring slots, field-major
 __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t W = a.W, G = a.G, R = a.R;
+    const uint32_t W = a.W, G = a.G, R = a.R, B = a.B;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t s = blockIdx.x;
     const uint32_t C = a.C, N = a.N;
-    const size_t cb = (size_t)s * C, nb = (size_t)s * N;
 
     uint4 *REC = reinterpret_cast<uint4 *>(smem);
     uint64_t *M = reinterpret_cast<uint64_t *>(REC + (size_t)W * G * 64);
@@ -128,12 +154,22 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     uint32_t *D = CNT + 8;
 
     for (uint32_t i = threadIdx.x; i < (W - 1) * 8 + 8; i += blockDim.x) CTL[i] = 0;
+    __syncthreads();
+    // Ticket order = start order: segment b of a scenario only ever waits on
+    // segments < b, which took earlier tickets, are already running, and never wait
+    // on b (global links are sized for every container) -- so the chain makes
+    // progress whatever the residency or dispatch order.
+    if (threadIdx.x == 0) CNT[4] = atomicAdd(a.ticket, 1u);
+    __syncthreads();
+    const uint32_t tk = __builtin_amdgcn_readfirstlane(CNT[4]);
+    const uint32_t s = tk / B, b = tk % B;
+    const size_t cb = (size_t)s * C, nb = (size_t)s * N;
 
     // ---- stage the tile into LDS and build the bucket masks ----
     // lane k < 32 holds Tc[k], lane 32 + k holds Tm[k] (K == 32: one wave covers both)
     static_assert(K == 32, "mask/threshold lane layout assumes K == 32");
     const uint32_t my_t = lane < (uint32_t)K ? a.tc[lane] : a.tm[lane - K];
-    const uint32_t gbase = w * G;                       // first group of this tile
+    const uint32_t gbase = (b * W + w) * G;             // first group of this tile
     uint4 *Rw = REC + (size_t)gbase * 64;
     uint64_t *Mw = M + (size_t)gbase * K * 2;
     uint32_t schedbits = 0, usedbits = 0;               // bit g for node (g, lane)
@@ -160,6 +196,13 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     __syncthreads();
 
     const bool has_out = w + 1 < W;
+    const bool g_in = w == 0 && b > 0;                  // input from segment b-1
+    const bool g_out = w + 1 == W && b + 1 < B;         // output to segment b+1
+    const size_t LSLOT = 6 * 64;                        // u32 per global slot
+    uint32_t *gin_head = a.ghead + ((size_t)s * (B - 1) + (b - 1)) * 32;
+    uint32_t *gin_data = a.gdata + ((size_t)s * (B - 1) + (b - 1)) * a.slots * LSLOT;
+    uint32_t *gout_head = a.ghead + ((size_t)s * (B - 1) + b) * 32;
+    uint32_t *gout_data = a.gdata + ((size_t)s * (B - 1) + b) * a.slots * LSLOT;
     uint32_t *octl = CTL + w * 8;
     uint32_t *ictl = CTL + (w - 1) * 8;
     uint32_t *odata = D + (size_t)w * R * NF * 64;
@@ -177,7 +220,43 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         ck_a = STAT_CLK();
         uint32_t cpu = 0, mem = 0, req = 0, conf = 0, idx = 0;
         bool valid = false;
-        if (w == 0) {
+        if (g_in) {
+            // poll the upstream segment's head (sc1), bounded; then sc1 payload loads
+            uint32_t n_sp = 0;
+            uint64_t t0 = 0;
+            bool got = false;
+            while (true) {
+                if (g_ld(gin_head) > itail) { got = true; break; }
+                if (g_ld(a.gabort) || lds_acq(abort_flag)) break;
+                if ((++n_sp & 255u) == 0) {
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (!t0) {
+                        t0 = now;
+                    } else if (now - t0 > SPIN_TICKS) {
+                        g_st(a.gabort, 1u);
+                        lds_rel(abort_flag, 1u);
+                        if (lane == 0) atomicMax(a.err, (uint32_t)(-FP_EDEVICE));
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            st_spin_in += n_sp;
+            if (!got) break;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+            const uint32_t *sd = gin_data + (size_t)itail * LSLOT;
+            const uint32_t n = g_ld(sd);
+            if (n & END) break;
+            valid = lane < n;
+            if (valid) {
+                cpu = g_ld(sd + 64 + lane);
+                mem = g_ld(sd + 128 + lane);
+                req = g_ld(sd + 192 + lane);
+                conf = g_ld(sd + 256 + lane);
+                idx = g_ld(sd + 320 + lane);
+            }
+            itail++;
+        } else if (w == 0) {
             if (k0 >= C) break;
             const uint32_t i = k0 + lane;
             valid = i < C;
@@ -338,6 +417,29 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         }
 #endif
         const bool fwd = valid && !((placed >> lane) & 1ull);
+        if (g_out) {
+            // append to the open global slot; publish each full slot (never blocks)
+            const uint64_t fm = __builtin_amdgcn_ballot_w64(fwd);
+            const uint32_t f = (uint32_t)__popcll(fm);
+            if (!f) continue;
+            const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+            if (fwd) {
+                uint32_t *sd = gout_data + (size_t)(ohead + (pos >= 64 ? 1 : 0)) * LSLOT;
+                const uint32_t p = pos & 63u;
+                g_st(sd + 64 + p, cpu); g_st(sd + 128 + p, mem); g_st(sd + 192 + p, req);
+                g_st(sd + 256 + p, conf); g_st(sd + 320 + p, idx);
+            }
+            if (ofill + f >= 64) {
+                if (lane == 0) g_st(gout_data + (size_t)ohead * LSLOT, 64u);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                ohead++;
+                if (lane == 0) g_st(gout_head, ohead);
+                ofill = ofill + f - 64;
+            } else {
+                ofill += f;
+            }
+            continue;
+        }
         if (!has_out) {
             if (fwd) {
                 a.assign[cb + idx] = FP_NONE;
@@ -377,6 +479,18 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     }
 
     // ---- flush + end of stream ----
+    if (g_out && !lds_acq(abort_flag)) {
+        if (ofill) {
+            if (lane == 0) g_st(gout_data + (size_t)ohead * LSLOT, ofill);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ohead++;
+            if (lane == 0) g_st(gout_head, ohead);
+        }
+        if (lane == 0) g_st(gout_data + (size_t)ohead * LSLOT, END);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ohead++;
+        if (lane == 0) g_st(gout_head, ohead);
+    }
     if (has_out && !lds_acq(abort_flag)) {
         bool ok = true;
         if (ofill) {
@@ -413,7 +527,23 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0 && a.cost) a.cost[s] = fpd::pack_cost(CNT[1], CNT[0], a.scen_base + s);
+    if (threadIdx.x == 0) {
+        a.part[((size_t)s * B + b) * 2] = CNT[0];
+        a.part[((size_t)s * B + b) * 2 + 1] = CNT[1];
+    }
+}
+
+// cost[s] from the per-segment partial counts (SPEC.md 2.4)
+__global__ void k_cost_reduce(uint32_t S, uint32_t B, uint32_t scen_base, const uint32_t *__restrict__ part,
+                              uint64_t *__restrict__ cost) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    uint32_t used = 0, rej = 0;
+    for (uint32_t b = 0; b < B; ++b) {
+        used += part[((size_t)s * B + b) * 2];
+        rej += part[((size_t)s * B + b) * 2 + 1];
+    }
+    cost[s] = fpd::pack_cost(rej, used, scen_base + s);
 }
 
 __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
@@ -460,37 +590,52 @@ static void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
     }
 }
 
-// Picks (G, W) for N nodes: prefer 8 stages (two waves per SIMD), then fewer or
-// more; false when one CU's LDS cannot hold the scenario.
-bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, size_t *lds_out) {
+// Pipeline geometry for N nodes: W waves (stages) of G groups per workgroup
+// (segment) and B segments per scenario.  One segment holds at most
+// MAX_SEG_GROUPS groups (LDS: 1 KiB of records + 512 B of masks per group).
+constexpr uint32_t MAX_SEG_GROUPS = 80;
+
+bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out) {
     const uint32_t NG = (N + 63) / 64;
     const size_t cap = 160 * 1024;
     if (NG == 0) {
-        *G_out = 1; *W_out = 1; *lds_out = lds_bytes(1, 1, 2);
+        *G_out = 1; *W_out = 1; *B_out = 1; *lds_out = lds_bytes(1, 1, 2);
         return true;
     }
     // FLEETPLACE_PIPE_W: force the stage count (tuning experiments only)
     static const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
+    const uint32_t B = (NG + MAX_SEG_GROUPS - 1) / MAX_SEG_GROUPS;
+    const uint32_t per_seg = (NG + B - 1) / B;
     for (uint32_t W : {8u, 4u, 2u, 1u, 12u, 16u}) {
         if (forced_w > 0 && W != (uint32_t)forced_w) continue;
-        if (W > NG && W > 1) continue;
-        const uint32_t G = (NG + W - 1) / W;
+        if (W > per_seg && W > 1) continue;
+        const uint32_t G = (per_seg + W - 1) / W;
         if (G > MAX_G) continue;
-        const uint32_t Wn = (NG + G - 1) / G;  // drop empty tail stages
+        const uint32_t Wn = (per_seg + G - 1) / G;  // drop empty tail stages
         const size_t lds = lds_bytes(Wn, G, 2);
         if (lds > cap) continue;
-        *G_out = G; *W_out = Wn; *lds_out = lds;
+        *G_out = G; *W_out = Wn; *B_out = B; *lds_out = lds;
         return true;
     }
     return false;
 }
 
+// Workspace bytes fp_pipe_launch takes (0 if the geometry does not fit).
+size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
+    uint32_t G, W, B;
+    size_t lds;
+    if (!fp_pipe_plan(N, &G, &W, &B, &lds)) return 0;
+    const size_t SC = (size_t)S * C, nlinks = (size_t)S * (B - 1), slots = (C + 63) / 64 + 2;
+    return 5 * SC * 4 + 256 + nlinks * 128 + (size_t)S * B * 8 + 8 + nlinks * slots * 6 * 64 * 4 + 8 * 256;
+}
+
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const fp_batch *b, uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
-    uint32_t G, W;
+    uint32_t G, W, B;
     size_t lds;
-    if (!fp_pipe_plan(N, &G, &W, &lds)) return FP_EOVERFLOW;
+    if (!fp_pipe_plan(N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
     if (C >= 0x80000000u) return FP_EOVERFLOW;
+    if ((uint64_t)S * B > 0xFFFFFFFFull) return FP_EOVERFLOW;
     // deepest ring (2..4 slots) that still fits the CU's LDS
     uint32_t R = 2;
     for (uint32_t r = 4; r > 2; --r)
@@ -498,12 +643,19 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     lds = lds_bytes(W, G, R);
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;
+    const uint32_t slots = (C + 63) / 64 + 2;
+    const size_t nlinks = (size_t)S * (B - 1);
     uint32_t *s_cpu = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_mem = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_req = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_conf = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_idx = (uint32_t *)fp_ws_take(c, SC * 4);
-    if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx) return FP_ENOMEM;
+    uint32_t *ctl = (uint32_t *)fp_ws_take(c, 256 + nlinks * 128);  // ticket, abort | heads
+    uint32_t *part = (uint32_t *)fp_ws_take(c, (size_t)S * B * 8 + 8);
+    uint32_t *gdata = nlinks ? (uint32_t *)fp_ws_take(c, nlinks * slots * 6 * 64 * 4) : nullptr;
+    if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx || !ctl || !part || (nlinks && !gdata))
+        return FP_ENOMEM;
+    FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * 128, st));
     {
         size_t g = (SC + 255) / 256;
         if (g > 16384) g = 16384;
@@ -513,6 +665,8 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     }
     PipeArgs a;
     a.C = C; a.N = N; a.scen_base = scen_base; a.W = W; a.G = G; a.R = R;
+    a.B = B; a.slots = slots; a.ticket = ctl; a.gabort = ctl + 32; a.ghead = ctl + 64; a.gdata = gdata;
+    a.part = part;
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
     a.assign = b->assign; a.reason = b->reason; a.cost = b->cost; a.err = c->d_err;
@@ -524,9 +678,13 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
-    k_ffd_pipe<<<S, W * 64, lds, st>>>(a);
+    k_ffd_pipe<<<(unsigned)(S * B), W * 64, lds, st>>>(a);
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
+    if (b->cost) {
+        k_cost_reduce<<<(S + 255) / 256, 256, 0, st>>>(S, B, scen_base, part, b->cost);
+        FP_HIP(hipGetLastError());
+    }
     return FP_OK;
 }
 

@@ -201,6 +201,46 @@ def test_config4_scenarios_full_size(planner, O):
     assert int(best.item()) == int(np.argmin(costs))
 
 
+# ---- segmented pipeline: N beyond one workgroup's LDS (> 80 groups of 64 nodes) ----
+@pytest.mark.parametrize("C,N,flags", [(20_000, 6_000, 7), (30_000, 20_000, 7), (2_000, 100_000, 7),
+                                       (60_000, 33_000, 3), (5_000, 5_121, 7)])
+def test_ffd_segments_vs_oracle(C, N, flags, planner, O):
+    """Segments of one scenario hand their unplaced containers downstream through
+    global rings; the plan must be the sequential first fit all the same."""
+    cont, nodes = O.gen_scenario(SEED + 3 * C + N, 1, C, N, flags)
+    _check_ffd(planner, O, cont, nodes)
+
+
+def test_ffd_segments_batch_and_cycles(planner, O):
+    S, C, N, base = 3, 4_000, 11_000, 17
+    conts, nodes, levels = [], [], []
+    rng = np.random.default_rng(5)
+    for s in range(S):
+        c, n = O.gen_scenario(SEED + 9, base + s, C, N, 7)
+        conts.append(c)
+        nodes.append(n)
+        levels.append(np.where(rng.random(C) < 0.01, NONE, 0).astype(np.uint32))
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    assign, reason, cost, after = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
+                                                      [cat(nodes, i) for i in range(5)],
+                                                      level=np.concatenate(levels), scen_base=base)
+    for s in range(S):
+        ea, er, eafter, _ = O.place(conts[s], nodes[s], level=levels[s])
+        assert np.array_equal(assign[s * C:(s + 1) * C], ea)
+        assert np.array_equal(reason[s * C:(s + 1) * C], er)
+        assert int(cost[s]) == O.cost(ea, N, base + s)
+        for i in (0, 1, 3):
+            assert np.array_equal(after[i][s * N:(s + 1) * N], eafter[i])
+
+
+def test_config3_full_size(planner, O):
+    """BASELINE config 3: 1M containers x 100k nodes with label anti-affinity, one
+    scenario (20 segments), bit-exact against the oracle at full size."""
+    cont, nodes = O.gen_scenario(SEED + 3, 0, 1_000_000, 100_000, 7)
+    assign, reason = _check_ffd(planner, O, cont, nodes)
+    assert (reason == 1).any() and (reason == 0).any()
+
+
 # ---- stage 2 feasibility --------------------------------------------------------------------
 def test_feasibility_golden(golden, planner, O):
     for case in golden["feasibility"]:
