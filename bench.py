@@ -88,7 +88,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
-    from fleetflow_amd import DevBatch, Planner
+    from fleetflow_amd import DevBatch, Planner, shard
     from fleetflow_amd._lib import FP_K_PLACE, FP_K_SORT
 
     S = args.scenarios_per_gpu
@@ -98,18 +98,17 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     planner.set_stream(stream.cuda_stream)
-    db = DevBatch.allocate(S, C, N, dev, scen_base=rank * S)
+    base, _ = shard.block(rank, world, S * world)
+    db = DevBatch.allocate(S, C, N, dev, scen_base=base)
     planner.dev_gen_batch(SEED, db, FLAGS)
     pristine = db.node_snapshot()
-    gathered = torch.empty(S * world, dtype=torch.int64, device=dev)
     best = torch.empty(1, dtype=torch.int32, device=dev)
 
     def step():
         db.restore_nodes(pristine)
         planner.dev_place_batch(db)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, db.cost)
-            planner.dev_argmin_cost(gathered, best)
+            planner.dev_argmin_cost(shard.gather_costs(db.cost, world, S * world), best)
         else:
             planner.dev_argmin_cost(db.cost, best)
 
