@@ -169,9 +169,9 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     // lane k < 32 holds Tc[k], lane 32 + k holds Tm[k] (K == 32: one wave covers both)
     static_assert(K == 32, "mask/threshold lane layout assumes K == 32");
     const uint32_t my_t = lane < (uint32_t)K ? a.tc[lane] : a.tm[lane - K];
-    const uint32_t gbase = (b * W + w) * G;             // first group of this tile
-    uint4 *Rw = REC + (size_t)gbase * 64;
-    uint64_t *Mw = M + (size_t)gbase * K * 2;
+    const uint32_t gbase = (b * W + w) * G;             // first (global) group of this tile
+    uint4 *Rw = REC + (size_t)w * G * 64;               // the tile's LDS records
+    uint64_t *Mw = M + (size_t)w * G * K * 2;           // and masks
     uint32_t schedbits = 0, usedbits = 0;               // bit g for node (g, lane)
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t n = (gbase + g) * 64 + lane;

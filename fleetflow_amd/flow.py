@@ -28,35 +28,83 @@ U32_MAX = 0xFFFFFFFF
 
 
 @dataclass
+class Port:
+    """fleetflow_core::Port (model/port.rs); parsed by parser/port.rs."""
+    host: int
+    container: int
+    protocol: str = "tcp"
+    host_ip: str | None = None
+
+
+@dataclass
+class Volume:
+    """fleetflow_core::Volume (model/volume.rs); parsed by parser/volume.rs."""
+    host: str
+    container: str
+    read_only: bool = False
+
+
+@dataclass
 class Service:
-    """fleetflow_core::Service subset (model/service.rs:26-70)."""
+    """fleetflow_core::Service subset (model/service.rs:26-70): the fields the plan
+    path and the dry-run presenter read."""
     image: str | None = None
     version: str | None = None
+    command: str | None = None
+    service_type: str | None = None
+    restart: str | None = None
+    registry: str | None = None
+    ports: list[Port] = field(default_factory=list)
+    environment: dict[str, str] = field(default_factory=dict)
+    volumes: list[Volume] = field(default_factory=list)
     depends_on: list[str] = field(default_factory=list)
     # SPEC.md 4 resource-request extension (ignored by the reference parser,
     # parser/service.rs:222); absent => unconstrained (0)
     cpu_m: int = 0
     mem_mib: int = 0
     labels: list[str] = field(default_factory=list)      # required "key=value" labels
-    host_ports: list[int] = field(default_factory=list)  # from ports{ port host=... }
     anti_affinity: str | None = None
+
+    @property
+    def host_ports(self) -> list[int]:
+        return [p.host for p in self.ports]
+
+    def merge(self, other: "Service") -> None:
+        """model/service.rs:380-428: Options override when set, Vecs when non-empty,
+        the environment map is merged with ``other`` winning."""
+        for f in ("service_type", "image", "version", "command", "restart", "registry", "anti_affinity"):
+            if getattr(other, f) is not None:
+                setattr(self, f, getattr(other, f))
+        for f in ("ports", "volumes", "depends_on", "labels"):
+            if getattr(other, f):
+                setattr(self, f, list(getattr(other, f)))
+        for f in ("cpu_m", "mem_mib"):
+            if getattr(other, f):
+                setattr(self, f, getattr(other, f))
+        self.environment.update(other.environment)
 
 
 @dataclass
 class Stage:
-    """fleetflow_core::Stage subset (model/stage.rs:48-64)."""
+    """fleetflow_core::Stage (model/stage.rs:48-64)."""
     services: list[str] = field(default_factory=list)
     servers: list[str] = field(default_factory=list)
+    variables: dict[str, str] = field(default_factory=dict)
+    registry: str | None = None
+    backend: str = "docker"
 
 
 @dataclass
 class Server:
-    """Node-table entry (controlplane model.rs:399-442 capacity/labels/scheduling)."""
+    """Node-table entry: KDL ``server`` (parser/cloud.rs:46-140) or a CP registry
+    row (controlplane model.rs:399-442 capacity/labels/scheduling)."""
     slug: str
     cpu_m: int = U32_MAX
     mem_mib: int = U32_MAX
     labels: list[str] = field(default_factory=list)
     schedulable: bool = True
+    provider: str = ""
+    plan: str | None = None
 
 
 @dataclass
@@ -66,6 +114,8 @@ class Flow:
     services: dict[str, Service] = field(default_factory=dict)
     stages: dict[str, Stage] = field(default_factory=dict)
     servers: dict[str, Server] = field(default_factory=dict)
+    registry: str | None = None
+    variables: dict[str, str] = field(default_factory=dict)
 
 
 _PLANNER: Planner | None = None

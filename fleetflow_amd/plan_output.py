@@ -1,0 +1,103 @@
+"""Plan output: JSON plan and the dry-run presenter.
+
+``plan_to_json`` is the machine form carried to the control plane next to
+``DeployRequest`` (crates/fleetflow-container/src/engine.rs:16-25):
+``{stage, order, levels, level_order, assign, rejected}``.
+
+``format_up_dry_run`` / ``format_deploy_dry_run`` reproduce the reference's
+``fleet up --dry-run`` (crates/fleetflow/src/commands/up.rs:57-136) and
+``fleet deploy --dry-run`` (crates/fleetflow/src/commands/deploy.rs:14-100)
+line for line, without ANSI colour. When a ``Plan`` is given, each service
+block gains two lines, its start level and its planned server. Without one the
+text is the reference's. The environment line lists variables in definition
+order (the reference iterates a HashMap, so its order is arbitrary; compare it
+as a set).
+"""
+from __future__ import annotations
+
+import json
+
+from .flow import U32_MAX, Flow, Plan
+from .parser import FlowError
+
+
+def plan_to_json(plan: Plan, indent: int | None = None) -> str:
+    """Serialise a plan; a cycle member's level is null (it was U32_MAX)."""
+    return json.dumps({
+        "stage": plan.stage,
+        "order": plan.order,
+        "levels": {k: (None if v == U32_MAX else v) for k, v in plan.levels.items()},
+        "level_order": plan.level_order,
+        "assign": plan.assignment,
+        "rejected": plan.rejected,
+    }, ensure_ascii=False, indent=indent)
+
+
+def plan_from_json(text: str) -> Plan:
+    d = json.loads(text)
+    return Plan(d["stage"], d["order"], {k: (U32_MAX if v is None else v) for k, v in d["levels"].items()},
+                d["level_order"], d["assign"], d["rejected"])
+
+
+def get_network_name(project: str, stage: str) -> str:
+    """crates/fleetflow-container/src/converter.rs:12-14."""
+    return f"{project}-{stage}"
+
+
+def is_sensitive_key(key: str) -> bool:
+    """crates/fleetflow/src/utils.rs:76-82."""
+    k = key.lower()
+    return "pass" in k or "secret" in k or "key" in k or "token" in k
+
+
+def _service_block(flow: Flow, stage: str, name: str, container_suffix: str, plan: Plan | None) -> list[str]:
+    svc = flow.services.get(name)
+    if svc is None:
+        raise FlowError(f"サービス '{name}' の定義が見つかりません")
+    lines = ["", f"  サービス: {name}",
+             f"    コンテナ: {flow.name}-{stage}-{name}{container_suffix}",
+             f"    イメージ: {svc.image if svc.image is not None else '(未設定)'}"]
+    for p in svc.ports:
+        lines.append(f"    ポート: {p.host} → {p.container}/{p.protocol}")
+    for v in svc.volumes:
+        lines.append(f"    ボリューム: {v.host} → {v.container} ({'ro' if v.read_only else 'rw'})")
+    if svc.environment:
+        env = [f"{k}=***" if is_sensitive_key(k) else f"{k}={v}" for k, v in svc.environment.items()]
+        lines.append(f"    環境変数: {', '.join(env)}")
+    if plan is not None:
+        lv = plan.levels.get(name)
+        lines.append(f"    起動レベル: {'CYCLE' if lv == U32_MAX else lv}")
+        if name in plan.assignment:
+            lines.append(f"    配置先: {plan.assignment[name]}")
+        elif name in plan.rejected:
+            lines.append(f"    配置先: (配置不可: {plan.rejected[name]})")
+        else:
+            lines.append("    配置先: local")
+    return lines
+
+
+_FOOTER = "[dry-run] 実際の操作は行われません。--dry-run を外して実行してください。"
+
+
+def format_up_dry_run(flow: Flow, stage_name: str, plan: Plan | None = None) -> str:
+    """up.rs:57-136 (``print_dry_run_plan``) over ``stage.services``."""
+    stage = flow.stages[stage_name]
+    lines = [f"[dry-run] ステージ '{stage_name}' の起動計画:", "",
+             f"  ネットワーク: {get_network_name(flow.name, stage_name)} (作成予定)"]
+    for name in stage.services:
+        lines += _service_block(flow, stage_name, name, "", plan)
+    lines += ["", _FOOTER]
+    return "\n".join(lines) + "\n"
+
+
+def format_deploy_dry_run(flow: Flow, stage_name: str, target_services: list[str], tenant_line: str,
+                          plan: Plan | None = None) -> str:
+    """deploy.rs:14-100 (``print_dry_run_plan``) over the filtered target
+    services; ``tenant_line`` is the already-resolved tenant description
+    (deploy.rs:475-485)."""
+    lines = [f"[dry-run] ステージ '{stage_name}' のデプロイ計画:", "", f"  テナント: {tenant_line}", "",
+             f"  ネットワーク: {get_network_name(flow.name, stage_name)} (作成予定)"]
+    for name in target_services:
+        lines += _service_block(flow, stage_name, name, " (停止・削除→再作成)", plan)
+    lines += ["", _FOOTER]
+    return "\n".join(lines) + "\n"

@@ -94,6 +94,54 @@ def test_dry_run_fixtures(kats, planner):
         assert plan.assignment == {} and plan.rejected == {}  # no servers -> "local"
 
 
+def test_dry_run_from_kdl(kats, planner):
+    """Config 1 end to end: fleet.kdl -> KDL front end -> GPU plan -> dry-run text."""
+    import os
+    from fleetflow_amd.flow import plan_stage
+    from fleetflow_amd.parser import parse_kdl_file
+    from fleetflow_amd.plan_output import format_up_dry_run, plan_from_json, plan_to_json
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = {"local": ("readme", 0), "default": ("hello-world", 1)}
+    for fx in kats["dry_run_fixtures"]:
+        proj, _ = files[fx["stage"]]
+        flow = parse_kdl_file(os.path.join(here, "golden", "kdl", proj, ".fleetflow", "fleet.kdl"))
+        assert flow.stages[fx["stage"]].services == fx["services"]
+        plan = plan_stage(flow, fx["stage"], planner)
+        assert plan.order == fx["order"]
+        assert [plan.levels[s] for s in fx["services"]] == fx["levels"]
+        assert plan.assignment == {} and plan.rejected == {}
+        assert plan_from_json(plan_to_json(plan)) == plan
+        text = format_up_dry_run(flow, fx["stage"], plan)
+        assert text.count("    配置先: local") == len(fx["services"])
+
+
+def test_plan_stage_with_registry_nodes(planner, O):
+    """Registry rows -> node table -> per-service fan-out, checked against the oracle."""
+    from fleetflow_amd.flow import Flow, LabelDict, Service, Stage, plan_stage
+    from fleetflow_amd.registry import node_table
+    rows = [{"slug": f"node-{i:02d}", "capacity": {"cpu_cores": 2 + i % 3, "memory_gb": 4 + 2 * (i % 2)},
+             "labels": {"region": "tokyo" if i % 2 else "osaka"}, "scheduling": "cordon" if i == 3 else None}
+            for i in range(6)]
+    nodes = node_table(rows)
+    svcs = {f"s{i}": Service(cpu_m=500 + 250 * (i % 5), mem_mib=1024 * (1 + i % 3),
+                             labels=["region=tokyo"] if i % 4 == 0 else [],
+                             anti_affinity="web" if i % 3 == 0 else None, depends_on=[f"s{i - 1}"] if i else [])
+            for i in range(20)}
+    flow = Flow(services=svcs, stages={"live": Stage(services=list(svcs))})
+    plan = plan_stage(flow, "live", planner, servers=nodes)
+    ld = LabelDict([lab for s in svcs.values() for lab in s.labels] + [lab for n in nodes for lab in n.labels])
+    cont = ([s.cpu_m for s in svcs.values()], [s.mem_mib for s in svcs.values()],
+            [ld.mask(s.labels) for s in svcs.values()], [(1 << 16) if s.anti_affinity else 0 for s in svcs.values()])
+    nd = ([n.cpu_m for n in nodes], [n.mem_mib for n in nodes], [ld.mask(n.labels) for n in nodes],
+          [0] * len(nodes), [int(n.schedulable) for n in nodes])
+    ea, er, _, _ = O.place(cont, nd, level=[plan.levels[s] for s in svcs])
+    for i, s in enumerate(svcs):
+        if ea[i] != NONE:
+            assert plan.assignment[s] == nodes[ea[i]].slug
+        else:
+            assert plan.rejected[s] == "NOFIT"
+
+
 # ---- A6 FFD ------------------------------------------------------------------------------
 def test_ffd_golden(golden, planner, O):
     for case in golden["ffd"]:
