@@ -166,7 +166,7 @@ def main():
                        "parallelism": f"scenario-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "kernel": "k_ffd (fp_place.hip)", "kernel_ms": kernel_s * 1e3,
+                         "kernel": "k_ffd_pipe (fp_pipe.hip)", "kernel_ms": kernel_s * 1e3,
                          "units_per_launch": evals_launch, "bytes_per_unit": 16},
             "breakdown_ms": {"ffd_kernel": place_ms / max(place_n, 1), "sort": sort_ms / max(sort_n, 1)},
             "best_scenario": best_id,
