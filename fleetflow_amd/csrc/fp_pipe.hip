@@ -50,7 +50,7 @@ constexpr uint32_t CYC = 0x80000000u;
 // launch with FP_EDEVICE.  Downstream stages legitimately wait for most of a long
 // launch, so the bound is wall-clock time, not an iteration count.
 constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s
-constexpr uint32_t MAX_G = 32;      // groups per stage (bit registers are u32)
+constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per group)
 constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
 constexpr int SB = 8;               // containers per corner sub-batch
 
@@ -134,21 +134,25 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t my_t, int bas
     return k;
 }
 
+// Node records (cpu_free, mem_free, conflict_used, labels) of a wave's tile live
+// in that wave's VGPRs: G compile-time groups, 4 registers each.  The prescan
+// reads them with static indices; the candidate loop reads and updates group g
+// (wave-uniform) through s_set_gpr_idx-indexed moves.  LDS then holds only the
+// masks and the rings, so two workgroups fit on one CU.
 // LDS layout (bytes; every region 16-aligned):
-//   REC : W*G*64 uint4          node records (cf, mf, cu, lab) of every tile
 //   M   : W*G*K*2 u64           B_cpu / B_mem interleaved per (g, k)
 //   CTL : (W-1)*8 u32 + 8 u32   per link [0]=head [1]=tail [2..2+R)=slot counts; then
 //                               CNT [0]=n_used [1]=n_rej [2]=abort
 //   D   : (W-1)*R*NF*64 u32     ring slots, field-major
+template <uint32_t G>
 __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t W = a.W, G = a.G, R = a.R, B = a.B;
+    const uint32_t W = a.W, R = a.R, B = a.B;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t C = a.C, N = a.N;
 
-    uint4 *REC = reinterpret_cast<uint4 *>(smem);
-    uint64_t *M = reinterpret_cast<uint64_t *>(REC + (size_t)W * G * 64);
+    uint64_t *M = reinterpret_cast<uint64_t *>(smem);
     uint32_t *CTL = reinterpret_cast<uint32_t *>(M + (size_t)W * G * K * 2);
     uint32_t *CNT = CTL + (W - 1) * 8;
     uint32_t *D = CNT + 8;
@@ -170,23 +174,26 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     static_assert(K == 32, "mask/threshold lane layout assumes K == 32");
     const uint32_t my_t = lane < (uint32_t)K ? a.tc[lane] : a.tm[lane - K];
     const uint32_t gbase = (b * W + w) * G;             // first (global) group of this tile
-    uint4 *Rw = REC + (size_t)w * G * 64;               // the tile's LDS records
-    uint64_t *Mw = M + (size_t)w * G * K * 2;           // and masks
+    uint64_t *Mw = M + (size_t)w * G * K * 2;           // the tile's masks
+    uint32_t rcf[G], rmf[G], rcu[G], rlab[G];           // the tile's node records
     uint32_t schedbits = 0, usedbits = 0;               // bit g for node (g, lane)
+#pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t n = (gbase + g) * 64 + lane;
         const bool in = n < N;
         const bool sc = in && a.sched[nb + n] != 0;
-        uint4 r;
-        r.x = in ? a.cf[nb + n] : 0u;
-        r.y = in ? a.mf[nb + n] : 0u;
-        r.z = in ? a.cu[nb + n] : 0u;
-        r.w = in ? a.lab[nb + n] : 0u;
-        Rw[g * 64 + lane] = r;
+        rcf[g] = in ? a.cf[nb + n] : 0u;
+        rmf[g] = in ? a.mf[nb + n] : 0u;
+        rcu[g] = in ? a.cu[nb + n] : 0u;
+        rlab[g] = in ? a.lab[nb + n] : 0u;
         schedbits |= sc ? (1u << g) : 0u;
+    }
+    for (uint32_t g = 0; g < G; ++g) {
+        const bool sc = (schedbits >> g) & 1u;
+        const uint32_t x = rcf[g], y = rmf[g];
         for (int k = 0; k < K; ++k) {  // every lane takes part in each ballot
-            const uint64_t bc = __builtin_amdgcn_ballot_w64(sc & (r.x >= __builtin_amdgcn_readlane(my_t, k)));
-            const uint64_t bm = __builtin_amdgcn_ballot_w64(sc & (r.y >= __builtin_amdgcn_readlane(my_t, K + k)));
+            const uint64_t bc = __builtin_amdgcn_ballot_w64(sc & (x >= __builtin_amdgcn_readlane(my_t, k)));
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(sc & (y >= __builtin_amdgcn_readlane(my_t, K + k)));
             if (lane == (uint32_t)k) {
                 Mw[((size_t)g * K + k) * 2] = bc;
                 Mw[((size_t)g * K + k) * 2 + 1] = bm;
@@ -323,13 +330,13 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             cqv[q] = (uint32_t)__shfl((int)qc, (int)(q * SB));
             mqv[q] = (uint32_t)__shfl((int)qm, (int)(q * SB));
         }
+#pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
-            const uint4 r = Rw[g * 64 + lane];
             const bool sc = (schedbits >> g) & 1u;
             uint64_t e = 0;  // E_{my_q}[g]
 #pragma unroll
             for (uint32_t q = 0; q < 64 / SB; ++q) {
-                const uint64_t eq = __builtin_amdgcn_ballot_w64(sc & (r.x >= cqv[q]) & (r.y >= mqv[q]));
+                const uint64_t eq = __builtin_amdgcn_ballot_w64(sc & (rcf[g] >= cqv[q]) & (rmf[g] >= mqv[q]));
                 e = my_q == q ? eq : e;
             }
             const uint64_t *mg = Mw + (size_t)g * K * 2;
@@ -346,15 +353,9 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
 #ifdef FP_PIPE_STATS
         const unsigned long long tl_pre = ck_b;
 #endif
-        // Exact first fit, container by container in FFD order.  The records of the
-        // last group touched stay in registers (g_reg, r_reg): consecutive containers
-        // mostly hit the same "frontier" group, so a placement there is a register
-        // update plus a fire-and-forget LDS write, with no LDS read to wait for.  LDS
-        // is re-read only when the candidate group changes (all writes go through
-        // r_reg first, so register and LDS copies never disagree).
+        // Exact first fit, container by container in FFD order; group g's records are
+        // read and written in registers through a wave-uniform index.
         {
-            uint32_t g_reg = 0xFFFFFFFFu;
-            uint4 r_reg = make_uint4(0u, 0u, 0u, 0u);
             while (todo) {
                 const uint32_t ti = (uint32_t)__builtin_ctzll(todo);
                 todo &= todo - 1;
@@ -366,27 +367,23 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                 while (cc) {
                     const uint32_t g = (uint32_t)__builtin_ctz(cc);
                     cc &= cc - 1;
-                    if (g != g_reg) {
-                        r_reg = Rw[g * 64 + lane];
-                        g_reg = g;
-                    }
+                    const uint32_t x = rcf[g], y = rmf[g], z = rcu[g], lb = rlab[g];
                     if (STAT_ON) st_checks++;
-                    const bool ok = ((schedbits >> g) & 1u) & (r_reg.x >= c_cpu) & (r_reg.y >= c_mem) &
-                                    ((r_reg.w & c_req) == c_req) & ((r_reg.z & c_conf) == 0u);
+                    const bool ok = ((schedbits >> g) & 1u) & (x >= c_cpu) & (y >= c_mem) &
+                                    ((lb & c_req) == c_req) & ((z & c_conf) == 0u);
                     const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
                     if (m) {
                         // placement, branch-free: lane l's record changes; one all-lane
                         // ds_and_b64 clears the crossed buckets (lanes 0-31 cpu masks,
                         // lanes 32-63 mem masks of group g)
                         const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                        const uint32_t oc = __builtin_amdgcn_readlane(r_reg.x, l);
-                        const uint32_t om = __builtin_amdgcn_readlane(r_reg.y, l);
+                        const uint32_t oc = __builtin_amdgcn_readlane(x, l);
+                        const uint32_t om = __builtin_amdgcn_readlane(y, l);
                         const uint32_t nc = oc - c_cpu, nm = om - c_mem;
                         const bool me = lane == l;
-                        r_reg.x = me ? nc : r_reg.x;
-                        r_reg.y = me ? nm : r_reg.y;
-                        r_reg.z = me ? (r_reg.z | c_conf) : r_reg.z;
-                        Rw[g * 64 + lane] = r_reg;
+                        rcf[g] = me ? nc : x;
+                        rmf[g] = me ? nm : y;
+                        rcu[g] = me ? (z | c_conf) : z;
                         const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
                         const bool crossed = (my_t <= ov) & (my_t > nv);
                         atomicAnd((unsigned long long *)&Mw[(size_t)g * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
@@ -516,14 +513,14 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     }
     (void)ck_t0; (void)ck_in; (void)ck_pre; (void)ck_cand; (void)ck_fwd; (void)ck_wait;
     (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
-    // write the tile's node state back (LDS -> HBM)
+    // write the tile's node state back (registers -> HBM)
+#pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t n = (gbase + g) * 64 + lane;
         if (n < N) {
-            const uint4 r = Rw[g * 64 + lane];
-            a.cf[nb + n] = r.x;
-            a.mf[nb + n] = r.y;
-            a.cu[nb + n] = r.z;
+            a.cf[nb + n] = rcf[g];
+            a.mf[nb + n] = rmf[g];
+            a.cu[nb + n] = rcu[g];
         }
     }
     __syncthreads();
@@ -567,9 +564,22 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
 }
 
 size_t lds_bytes(uint32_t W, uint32_t G, uint32_t R) {
-    return (size_t)W * G * 64 * 16 + (size_t)W * G * K * 16 + ((size_t)(W - 1) * 8 + 8) * 4 +
-           (size_t)(W - 1) * R * NF * 64 * 4;
+    return (size_t)W * G * K * 16 + ((size_t)(W - 1) * 8 + 8) * 4 + (size_t)(W - 1) * R * NF * 64 * 4;
 }
+
+// G is a template parameter (records are register arrays); one instantiation per G
+template <uint32_t G>
+static int launch_g(hipStream_t st, unsigned grid, unsigned block, size_t lds, const PipeArgs &a) {
+    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe<G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_ffd_pipe<G><<<grid, block, lds, st>>>(a);
+    return FP_OK;
+}
+
+typedef int (*launch_fn)(hipStream_t, unsigned, unsigned, size_t, const PipeArgs &);
+static const launch_fn kLaunch[MAX_G + 1] = {
+    nullptr,         launch_g<1>,  launch_g<2>,  launch_g<3>,  launch_g<4>,  launch_g<5>,
+    launch_g<6>,     launch_g<7>,  launch_g<8>,  launch_g<9>,  launch_g<10>, launch_g<11>,
+    launch_g<12>,    launch_g<13>, launch_g<14>, launch_g<15>, launch_g<16>};
 
 }  // namespace fpp
 
@@ -592,8 +602,10 @@ static void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
 
 // Pipeline geometry for N nodes: W waves (stages) of G groups per workgroup
 // (segment) and B segments per scenario.  One segment holds at most
-// MAX_SEG_GROUPS groups (LDS: 1 KiB of records + 512 B of masks per group).
+// MAX_SEG_GROUPS groups: 8 stages x 10 groups keeps a workgroup at <= 80 KB of
+// LDS (512 B of masks per group + rings), so two workgroups share a CU.
 constexpr uint32_t MAX_SEG_GROUPS = 80;
+constexpr size_t LDS_HALF_CU = 80 * 1024;
 
 bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out) {
     const uint32_t NG = (N + 63) / 64;
@@ -636,10 +648,10 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     if (!fp_pipe_plan(N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
     if (C >= 0x80000000u) return FP_EOVERFLOW;
     if ((uint64_t)S * B > 0xFFFFFFFFull) return FP_EOVERFLOW;
-    // deepest ring (2..4 slots) that still fits the CU's LDS
+    // deepest ring (2..4 slots) that keeps two workgroups per CU (else one)
     uint32_t R = 2;
     for (uint32_t r = 4; r > 2; --r)
-        if (lds_bytes(W, G, r) <= 160 * 1024) { R = r; break; }
+        if (lds_bytes(W, G, r) <= LDS_HALF_CU) { R = r; break; }
     lds = lds_bytes(W, G, R);
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;
@@ -675,10 +687,11 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     // only decides how tight the candidate masks are)
     fp_thresholds(minc, maxc, a.tc);
     fp_thresholds(minm, maxm, a.tm);
-    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (G < 1 || G > MAX_G) return FP_EOVERFLOW;
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
-    k_ffd_pipe<<<(unsigned)(S * B), W * 64, lds, st>>>(a);
+    int rc = kLaunch[G](st, (unsigned)(S * B), W * 64, lds, a);
+    if (rc) return rc;
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
     if (b->cost) {

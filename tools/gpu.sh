@@ -1,10 +1,10 @@
 #!/bin/bash
 # Run a command on the GPU box via gpurun; retry ONLY when gpurun reports that the
-# box never ran it (status=transient / exit 3), at most 4 attempts, sleeping for the
+# box never ran it (status=transient / exit 3), at most 8 attempts, sleeping for the
 # back-off gpurun advertises ("retry in Ns").  A command that ran and failed is never
 # retried.
 set -u
-for attempt in 1 2 3 4; do
+for attempt in 1 2 3 4 5 6 7 8; do
   out=$(/usr/local/graft/bin/gpurun "$@" 2>&1); rc=$?
   echo "$out" | tail -4
   if echo "$out" | grep -q "status=transient" || [ $rc -eq 3 ]; then
