@@ -1,13 +1,15 @@
 // fp_pipe.hip -- stage 3 FFD as an intra-workgroup tile pipeline (SPEC.md 2.3).
 //
-// One workgroup = one scenario.  Its N nodes are cut into W tiles of G groups of
-// 64 nodes; wave w owns tile w.  Node records (cpu_free, mem_free,
-// conflict_used, labels) live in LDS as 16-byte AoS records, so a wave checks a
-// whole 64-node group with one ds_read_b128 per lane and a wavefront ballot
-// (lowest set lane = first fit inside the group).  Containers stream through the
-// waves in FFD order: wave 0 reads the sorted container list from HBM, places
-// what fits its tile and forwards the rest, in order, to wave 1 through an LDS
-// ring, and so on; what the last wave cannot place is NOFIT.
+// A scenario's N nodes are cut into tiles of G groups of 64 nodes; one wave (a
+// pipeline stage) owns a tile, W stages form a workgroup (a segment) and B
+// segments cover the scenario.  A stage keeps its tile's node records (cpu_free,
+// mem_free, conflict_used, labels) in VGPRs, so it checks a whole 64-node group
+// with a wavefront ballot (lowest set lane = first fit inside the group).
+// Containers stream through the stages in FFD order: stage 0 reads the sorted
+// container list from HBM, places what fits its tile and forwards the rest, in
+// order, to the next stage -- through an LDS ring inside a workgroup, through an
+// unbounded global ring between segments; what the last stage cannot place is
+// NOFIT.
 //
 // Exactness: a container lands in the first tile holding a feasible node, and a
 // tile's state only depends on the containers that reached it, in FFD order --
@@ -52,7 +54,10 @@ constexpr uint32_t CYC = 0x80000000u;
 constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s
 constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per group)
 constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
-constexpr int SB = 8;               // containers per corner sub-batch
+#ifndef FP_SB
+#define FP_SB 64
+#endif
+constexpr int SB = FP_SB;           // containers per corner sub-batch
 
 struct PipeArgs {
     uint32_t C, N, scen_base, W, G, R;
@@ -114,7 +119,10 @@ __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_
                 return false;
             }
         }
-        __builtin_amdgcn_s_sleep(1);
+        // back off: a spinning wave still takes issue slots from its CU's busy waves
+        if (n < 8) __builtin_amdgcn_s_sleep(1);
+        else if (n < 32) __builtin_amdgcn_s_sleep(4);
+        else __builtin_amdgcn_s_sleep(12);
     }
 }
 
@@ -246,7 +254,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                         break;
                     }
                 }
-                __builtin_amdgcn_s_sleep(2);
+                if (n_sp < 8) __builtin_amdgcn_s_sleep(2);
+                else __builtin_amdgcn_s_sleep(12);
             }
             st_spin_in += n_sp;
             if (!got) break;
@@ -312,7 +321,10 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         //  * per-container bucket masks B_cpu[g][kc] & B_mem[g][km];
         //  * an exact 2-D "corner" mask per sub-batch q of SB consecutive containers:
         //    E_q[g] = {l : sched && cpu_free >= min cpu(q) && mem_free >= min mem(q)}.
-        //    FFD order makes sub-batches homogeneous, so the corner is tight.
+        //    FFD order makes a batch's cpu range narrow, so the corner is tight in
+        //    cpu.  SB = 64 (one corner per batch, one ballot per group) ran the
+        //    config-4 bench 12% faster than SB = 8 (1.64 vs 1.96 checks per
+        //    container, but an 8x cheaper prescan on every stage a container visits).
         const uint32_t vc = valid ? cpu : 0xFFFFFFFFu, vm = valid ? mem : 0xFFFFFFFFu;
         uint32_t qc = vc, qm = vm;  // min over the lane's sub-batch (xor butterfly)
 #pragma unroll
@@ -602,9 +614,12 @@ static void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
 
 // Pipeline geometry for N nodes: W waves (stages) of G groups per workgroup
 // (segment) and B segments per scenario.  One segment holds at most
-// MAX_SEG_GROUPS groups: 8 stages x 10 groups keeps a workgroup at <= 80 KB of
-// LDS (512 B of masks per group + rings), so two workgroups share a CU.
-constexpr uint32_t MAX_SEG_GROUPS = 80;
+// MAX_SEG_GROUPS groups: 4 stages x 10 groups (20 KB of masks + rings).  Measured
+// on the config-4 bench (512 x 50k x 5k): 2 segments of 4 stages ran 16.0 ms, one
+// segment of 8 stages 17.1 ms, 4 x 2 16.7 ms, 8 x 1 17.1 ms -- the unbounded
+// global link decouples the halves better than a 2-4 slot LDS ring, and more
+// than ~4 segments adds link latency to the FFD chain.
+constexpr uint32_t MAX_SEG_GROUPS = 40;
 constexpr size_t LDS_HALF_CU = 80 * 1024;
 
 bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out) {
@@ -616,9 +631,12 @@ bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out,
     }
     // FLEETPLACE_PIPE_W: force the stage count (tuning experiments only)
     static const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
-    const uint32_t B = (NG + MAX_SEG_GROUPS - 1) / MAX_SEG_GROUPS;
+    // FLEETPLACE_PIPE_SEG: groups per segment (tuning experiments only)
+    static const int forced_seg = getenv("FLEETPLACE_PIPE_SEG") ? atoi(getenv("FLEETPLACE_PIPE_SEG")) : 0;
+    const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg : MAX_SEG_GROUPS;
+    const uint32_t B = (NG + seg_groups - 1) / seg_groups;
     const uint32_t per_seg = (NG + B - 1) / B;
-    for (uint32_t W : {8u, 4u, 2u, 1u, 12u, 16u}) {
+    for (uint32_t W : {4u, 8u, 2u, 1u, 12u, 16u}) {
         if (forced_w > 0 && W != (uint32_t)forced_w) continue;
         if (W > per_seg && W > 1) continue;
         const uint32_t G = (per_seg + W - 1) / W;

@@ -310,3 +310,12 @@ def test_feasibility_random_vs_oracle(C, N, planner, O):
     first, count, bm = planner.feasibility(cont, nodes)
     ef, ec, eb = O.feasibility(cont, nodes)
     assert np.array_equal(first, ef) and np.array_equal(count, ec) and np.array_equal(bm, eb)
+
+
+# ---- pipeline geometry edges: 40 groups (2560 nodes) per segment, 10 per stage ----------
+@pytest.mark.parametrize("C,N,flags", [(4000, 640, 7), (4000, 641, 7), (7000, 2560, 7), (7000, 2561, 7),
+                                       (5000, 5120, 7), (3000, 5121, 3)])
+def test_ffd_geometry_edges(C, N, flags, planner, O):
+    """Stage (640 nodes), segment (2560) and two-segment (5120) boundaries."""
+    cont, nodes = O.gen_scenario(SEED + 13 * C + N, 3, C, N, flags)
+    _check_ffd(planner, O, cont, nodes)

@@ -1,0 +1,5 @@
+set -e
+for v in "" _sb16 _sb32 _sb64; do
+  FLEETPLACE_LIB=$PWD/fleetflow_amd/libfleetplace$v.so timeout -k 10 120 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/exp_sb$v.json 2>/dev/null
+  python -c "import json;d=json.load(open('gpurun_out/exp_sb$v.json'));print('lib$v', d['roofline']['kernel_ms'], d['ms_per_step'])"
+done
