@@ -131,12 +131,14 @@ __global__ void k_lvl_init(const uint8_t *__restrict__ hd, const uint32_t *__res
     if (src) frontier[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)v;
 }
 
-// One thread per frontier vertex; relax its out-edges.
-__global__ void k_expand(const uint32_t *__restrict__ frontier, const uint32_t *__restrict__ fsize_p,
+// One thread per frontier vertex; relax its out-edges.  Level L's frontier size
+// is read from cnt[L] on the device and level L+1's is counted into cnt[L+1], so
+// the host enqueues levels without reading anything back (no per-level sync).
+__global__ void k_expand(const uint32_t *__restrict__ frontier, const uint32_t *__restrict__ cnt_l,
                          const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
                          uint32_t *__restrict__ level, uint32_t *__restrict__ indeg,
-                         uint32_t *__restrict__ next, uint32_t *__restrict__ ncount) {
-    const uint32_t fsize = *fsize_p;
+                         uint32_t *__restrict__ next, uint32_t *__restrict__ cnt_next) {
+    const uint32_t fsize = *cnt_l;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < fsize;
          i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t u = frontier[i];
@@ -145,7 +147,7 @@ __global__ void k_expand(const uint32_t *__restrict__ frontier, const uint32_t *
         for (uint32_t e = row_ptr[u]; e < e1; ++e) {
             const uint32_t v = col[e];
             atomicMax(&level[v], lu1);
-            if (atomicSub(&indeg[v], 1u) == 1u) next[atomicAdd(ncount, 1u)] = v;
+            if (atomicSub(&indeg[v], 1u) == 1u) next[atomicAdd(cnt_next, 1u)] = v;
         }
     }
 }
@@ -211,7 +213,9 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     size_t sort_tmp = 0;
     FP_HIP(rocprim::radix_sort_pairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                      (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)V, 0, 32, st));
-    int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + sort_tmp + 16 * 256);
+    // cnt[L] = frontier size of level L (one counter per possible level: <= V + 1)
+    const size_t ncnt = (size_t)V + 2;
+    int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + 16 * 256);
     if (rc) return rc;
     fp_ws_reset(c);
     uint32_t *indeg = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
@@ -220,14 +224,16 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     uint32_t *keys = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
     uint32_t *keys_out = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
     uint32_t *vals = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
-    uint32_t *cnts = (uint32_t *)fp_ws_take(c, 64);  // [0]=count A, [1]=count B, [2]=ncyc
+    uint32_t *cnt = (uint32_t *)fp_ws_take(c, ncnt * 4);
+    uint32_t *ncyc = (uint32_t *)fp_ws_take(c, 64);
     void *tmp = fp_ws_take(c, sort_tmp + 16);
-    if (!indeg || !fa || !fb || !keys || !keys_out || !vals || !cnts || !tmp) return FP_ENOMEM;
+    if (!indeg || !fa || !fb || !keys || !keys_out || !vals || !cnt || !ncyc || !tmp) return FP_ENOMEM;
 
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_LEVEL, &ev);
     FP_HIP(hipMemsetAsync(indeg, 0, (size_t)V * 4, st));
-    FP_HIP(hipMemsetAsync(cnts, 0, 64, st));
+    FP_HIP(hipMemsetAsync(cnt, 0, ncnt * 4, st));
+    FP_HIP(hipMemsetAsync(ncyc, 0, 64, st));
     k_check_csr<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, V, E, c->d_err);
     FP_HIP(hipGetLastError());
     if (E) {
@@ -235,35 +241,41 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
             g->col, E, V, indeg, c->d_err);
         FP_HIP(hipGetLastError());
     }
-    k_lvl_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, V, level, fa, &cnts[0]);
+    k_lvl_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, V, level, fa, &cnt[0]);
     FP_HIP(hipGetLastError());
     // corrupt CSR => stop before expanding
     FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
-    FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &cnts[0], 4, hipMemcpyDeviceToHost, st));
+    FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &cnt[0], 4, hipMemcpyDeviceToHost, st));
     FP_HIP(hipStreamSynchronize(st));
     if (((uint32_t *)c->h_small)[0]) return -(int)((uint32_t *)c->h_small)[0];
-    uint32_t fsize = ((uint32_t *)c->h_small)[2];
-    uint32_t *cur = fa, *nxt = fb, *ccnt = &cnts[0], *ncnt = &cnts[1];
-    uint32_t iters = 0;
-    while (fsize) {
-        FP_HIP(hipMemsetAsync(ncnt, 0, 4, st));
-        const unsigned grid = blocks_for(fsize, 256);
-        k_expand<<<grid, 256, 0, st>>>(cur, ccnt, g->row_ptr, g->col, level, indeg, nxt, ncnt);
-        FP_HIP(hipGetLastError());
-        FP_HIP(hipMemcpyAsync(c->h_small, ncnt, 4, hipMemcpyDeviceToHost, st));
-        FP_HIP(hipStreamSynchronize(st));
-        fsize = ((uint32_t *)c->h_small)[0];
-        uint32_t *t = cur; cur = nxt; nxt = t;
-        uint32_t *tc = ccnt; ccnt = ncnt; ncnt = tc;
-        ++iters;
+    const uint32_t f0 = ((uint32_t *)c->h_small)[2];
+    // Levels are enqueued in chunks of kChunk launches with no read-back in between
+    // (a level whose frontier is empty is a no-op launch); one read of the last
+    // chunk's final counter decides whether another chunk is needed.  The grid is
+    // sized for the widest possible frontier and grid-strides.
+    constexpr uint32_t kChunk = 64;
+    const unsigned grid = blocks_for(V, 256) < 256 ? blocks_for(V, 256) : 256;
+    uint32_t L = 0;  // levels enqueued so far
+    if (f0) {
+        while (true) {
+            for (uint32_t k = 0; k < kChunk && L + 1 < ncnt; ++k, ++L) {
+                uint32_t *cur = (L & 1) ? fb : fa, *nxt = (L & 1) ? fa : fb;
+                k_expand<<<grid, 256, 0, st>>>(cur, &cnt[L], g->row_ptr, g->col, level, indeg, nxt, &cnt[L + 1]);
+                FP_HIP(hipGetLastError());
+            }
+            FP_HIP(hipMemcpyAsync(c->h_small, &cnt[L], 4, hipMemcpyDeviceToHost, st));
+            FP_HIP(hipStreamSynchronize(st));
+            if (((uint32_t *)c->h_small)[0] == 0 || L + 1 >= ncnt) break;
+        }
     }
+    const uint32_t iters = L;
     // levels <= iters + 1; cycle key sorts after every level
     const uint32_t cyc_key = iters + 2;
-    k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, &cnts[2]);
+    k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, ncyc);
     FP_HIP(hipGetLastError());
     FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys, keys_out, vals, order, (size_t)V, 0,
                                      fp_bitwidth(cyc_key), st));
-    if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, &cnts[2], 4, hipMemcpyDeviceToDevice, st));
+    if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
     fp_prof_end(c, FP_K_LEVEL, ev);
     return FP_OK;
 }
