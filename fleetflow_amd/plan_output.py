@@ -101,3 +101,57 @@ def format_deploy_dry_run(flow: Flow, stage_name: str, target_services: list[str
         lines += _service_block(flow, stage_name, name, " (停止・削除→再作成)", plan)
     lines += ["", _FOOTER]
     return "\n".join(lines) + "\n"
+
+
+# ---- ordering consumers -------------------------------------
+
+def start_waves(plan: Plan) -> list[list[str]]:
+    """Parallel start waves for ``DeployEngine::create_and_start``
+    (crates/fleetflow-container/src/engine.rs:355-452 starts services one by one in
+    ``order_by_dependencies`` order).  Wave k holds the stage's services at level k
+    in declaration order; every dependency of a wave-k service is in an earlier
+    wave, so a wave's containers may be created and started concurrently (one
+    ``join_all`` per wave).  Levels that no service has are skipped.  CYCLE
+    services (level U32_MAX) are in no wave: the reference would start them in
+    bucket 2 (engine.rs:83); the plan reports them in ``plan.rejected``."""
+    by_level: dict[int, list[str]] = {}
+    seen = set()
+    for name in plan.level_order:
+        lv = plan.levels[name]
+        if lv == U32_MAX or name in seen:
+            continue
+        seen.add(name)
+        by_level.setdefault(lv, []).append(name)
+    return [by_level[k] for k in sorted(by_level)]
+
+
+def unit_base_name(project: str, stage: str, service: str) -> str:
+    """crates/fleetflow-container/src/quadlet.rs ``unit_base_name``: ``{project}-{stage}-{service}``."""
+    return f"{project}-{stage}-{service}"
+
+
+def quadlet_ordering_lines(project: str, stage: str, depends_on: list[str]) -> list[str]:
+    """``[Unit]`` ordering of a generated ``.container`` unit, as the reference emits
+    it (crates/fleetflow-container/src/quadlet.rs:95-100): for each dependency, in
+    ``depends_on`` order, ``After=`` and ``Requires=`` on its generated service."""
+    out = []
+    for dep in depends_on:
+        unit = f"{unit_base_name(project, stage, dep)}.service"
+        out += [f"After={unit}", f"Requires={unit}"]
+    return out
+
+
+def compose_depends_on_lines(depends_on: list[str]) -> list[str]:
+    """``depends_on:`` block of a compose service (crates/fleetflow-container/src/compose.rs:156-162);
+    names are YAML-quoted by the reference only when they need it, which service
+    names never do."""
+    if not depends_on:
+        return []
+    return ["    depends_on:"] + [f"      - {d}" for d in depends_on]
+
+
+def wave_start_script(plan: Plan, project: str) -> list[str]:
+    """Human-readable start schedule: one line per wave with its containers
+    (``{project}-{stage}-{service}``, up.rs:79 naming)."""
+    return [f"  wave {i}: " + ", ".join(f"{project}-{plan.stage}-{s}" for s in wave)
+            for i, wave in enumerate(start_waves(plan))]

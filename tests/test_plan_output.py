@@ -57,3 +57,60 @@ def test_plan_json_roundtrip():
 def test_sensitive_keys():
     assert [is_sensitive_key(k) for k in ["DB_PASSWORD", "api_key", "TOKEN", "SECRET_X", "USER"]] == [
         True, True, True, True, False]
+
+
+# ---- ordering consumers ----------------------------------------
+def test_start_waves_group_levels_in_declaration_order():
+    from fleetflow_amd.plan_output import start_waves, wave_start_script
+    # README fixture shape: postgres, redis (level 0) then app (level 1); a cycle pair is left out
+    plan = Plan("local", ["postgres", "redis", "app", "x", "y"],
+                {"postgres": 0, "redis": 0, "app": 1, "x": U32_MAX, "y": U32_MAX},
+                ["postgres", "redis", "app", "x", "y"], {}, {"x": "CYCLE", "y": "CYCLE"})
+    assert start_waves(plan) == [["postgres", "redis"], ["app"]]
+    assert wave_start_script(plan, "readme") == ["  wave 0: readme-local-postgres, readme-local-redis",
+                                                 "  wave 1: readme-local-app"]
+    # a level with no service (deps outside the stage put a root at level 1) is skipped
+    plan2 = Plan("s", ["b", "a"], {"a": 1, "b": 3}, ["a", "b"], {}, {})
+    assert start_waves(plan2) == [["a"], ["b"]]
+
+
+def test_start_waves_respect_every_dependency():
+    """Every depends_on edge inside the stage goes from an earlier wave to a later one."""
+    import numpy as np
+    from oracle import pyoracle as P
+    from fleetflow_amd.plan_output import start_waves
+    rng = np.random.default_rng(3)
+    names = [f"s{i}" for i in range(60)]
+    deps = {n: [names[j] for j in rng.integers(0, i, rng.integers(0, 3))] if i else [] for i, n in enumerate(names)}
+    # levels from the pure-Python oracle twin over the reversed CSR
+    V = len(names)
+    idx = {n: i for i, n in enumerate(names)}
+    rows = [[] for _ in range(V)]
+    for n in names:
+        for d in deps[n]:
+            rows[idx[d]].append(idx[n])
+    row_ptr = [0]
+    col = []
+    for r in rows:
+        col += r
+        row_ptr.append(len(col))
+    has_deps = [1 if deps[n] else 0 for n in names]
+    level, order = P.levelize(V, row_ptr, col, has_deps)
+    plan = Plan("s", names, {n: int(level[i]) for i, n in enumerate(names)},
+                [names[i] for i in order], {}, {})
+    wave_of = {n: w for w, wave in enumerate(start_waves(plan)) for n in wave}
+    assert sorted(wave_of) == sorted(names)
+    for n in names:
+        for d in deps[n]:
+            assert wave_of[d] < wave_of[n]
+
+
+def test_quadlet_and_compose_ordering_match_reference_emitters():
+    """quadlet.rs:529-540 (After=/Requires= per dependency) and compose.rs:156-162."""
+    from fleetflow_amd.plan_output import compose_depends_on_lines, quadlet_ordering_lines
+    lines = quadlet_ordering_lines("myapp", "live", ["db", "redis"])
+    assert lines == ["After=myapp-live-db.service", "Requires=myapp-live-db.service",
+                     "After=myapp-live-redis.service", "Requires=myapp-live-redis.service"]
+    assert quadlet_ordering_lines("myapp", "live", []) == []
+    assert compose_depends_on_lines(["db"]) == ["    depends_on:", "      - db"]
+    assert compose_depends_on_lines([]) == []
