@@ -381,9 +381,13 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                     cc &= cc - 1;
                     const uint32_t x = rcf[g], y = rmf[g], z = rcu[g], lb = rlab[g];
                     if (STAT_ON) st_checks++;
-                    const bool ok = ((schedbits >> g) & 1u) & (x >= c_cpu) & (y >= c_mem) &
-                                    ((lb & c_req) == c_req) & ((z & c_conf) == 0u);
-                    const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+                    // one v_cmp per condition straight into a scalar mask, ANDed on the
+                    // SALU (a single ballot of the combined bool costs two extra
+                    // dependent VALU ops on the chain)
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
+                                       __builtin_amdgcn_ballot_w64((lb & c_req) == c_req) &
+                                       __builtin_amdgcn_ballot_w64((z & c_conf) == 0u) &
+                                       __builtin_amdgcn_ballot_w64(((schedbits >> g) & 1u) != 0u);
                     if (m) {
                         // placement, branch-free: lane l's record changes; one all-lane
                         // ds_and_b64 clears the crossed buckets (lanes 0-31 cpu masks,
