@@ -14,25 +14,51 @@
 
 namespace {
 
-// out[0..1] = max(cpu), max(mem); out[2..3] = min positive cpu, mem (0xFFFFFFFF if none)
-__global__ void k_key_bounds(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
-                             size_t n, uint32_t *__restrict__ out /* [4] */) {
+// out[0..1] = max(cpu), max(mem); out[2..3] = min positive cpu, mem (0xFFFFFFFF if none).
+// 16-byte loads, a block-level reduction in LDS and one set of atomics per block.
+__device__ __forceinline__ void bounds_acc(uint32_t c, uint32_t m, uint32_t &mc, uint32_t &mm, uint32_t &lc,
+                                           uint32_t &lm) {
+    mc = max(mc, c);
+    mm = max(mm, m);
+    lc = c ? min(lc, c) : lc;
+    lm = m ? min(lm, m) : lm;
+}
+
+__global__ __launch_bounds__(256) void k_key_bounds(const uint32_t *__restrict__ cpu,
+                                                    const uint32_t *__restrict__ mem, size_t n,
+                                                    uint32_t *__restrict__ out /* [4] */) {
     uint32_t mc = 0, mm = 0, lc = 0xFFFFFFFFu, lm = 0xFFFFFFFFu;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t c = cpu[i], m = mem[i];
-        mc = max(mc, c);
-        mm = max(mm, m);
-        if (c) lc = min(lc, c);
-        if (m) lm = min(lm, m);
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(cpu) | reinterpret_cast<uintptr_t>(mem)) & 15u) == 0;
+    size_t head = 0;
+    if (aligned) {
+        const size_t n4 = n / 4;
+        const uint4 *c4 = reinterpret_cast<const uint4 *>(cpu), *m4 = reinterpret_cast<const uint4 *>(mem);
+        for (size_t i = t; i < n4; i += stride) {
+            const uint4 c = c4[i], m = m4[i];
+            bounds_acc(c.x, m.x, mc, mm, lc, lm);
+            bounds_acc(c.y, m.y, mc, mm, lc, lm);
+            bounds_acc(c.z, m.z, mc, mm, lc, lm);
+            bounds_acc(c.w, m.w, mc, mm, lc, lm);
+        }
+        head = n4 * 4;
     }
+    for (size_t i = head + t; i < n; i += stride) bounds_acc(cpu[i], mem[i], mc, mm, lc, lm);
     for (int o = 32; o > 0; o >>= 1) {
         mc = max(mc, (uint32_t)__shfl_xor((int)mc, o));
         mm = max(mm, (uint32_t)__shfl_xor((int)mm, o));
         lc = min(lc, (uint32_t)__shfl_xor((int)lc, o));
         lm = min(lm, (uint32_t)__shfl_xor((int)lm, o));
     }
-    if ((threadIdx.x & 63) == 0) {
+    __shared__ uint32_t red[4][4];
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[w][0] = mc; red[w][1] = mm; red[w][2] = lc; red[w][3] = lm; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t q = 1; q < blockDim.x / 64; ++q) {
+            mc = max(mc, red[q][0]); mm = max(mm, red[q][1]); lc = min(lc, red[q][2]); lm = min(lm, red[q][3]);
+        }
         atomicMax(&out[0], mc);
         atomicMax(&out[1], mm);
         atomicMin(&out[2], lc);
@@ -134,7 +160,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     fp_prof_begin(c, FP_K_SORT, &ev);
     FP_HIP(hipMemsetAsync(bounds, 0, 8, st));
     FP_HIP(hipMemsetAsync(bounds + 2, 0xFF, 8, st));
-    k_key_bounds<<<grid_for(SC, 256) < 1024 ? grid_for(SC, 256) : 1024, 256, 0, st>>>(
+    k_key_bounds<<<grid_for((SC + 3) / 4, 256) < 2048 ? grid_for((SC + 3) / 4, 256) : 2048, 256, 0, st>>>(
         b->cpu_m, b->mem_mib, SC, bounds);
     FP_HIP(hipGetLastError());
     FP_HIP(hipMemcpyAsync(c->h_small, bounds, 16, hipMemcpyDeviceToHost, st));
@@ -146,6 +172,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     const uint64_t cmax = cbits ? ((cbits == 64 ? ~0ull : ((1ull << cbits) - 1))) : 0ull;
     const uint64_t mmax = mbits ? ((1ull << mbits) - 1) : 0ull;
     const uint32_t *order = nullptr;
+    const uint64_t *skeys = nullptr;
     if (kbits == 0) {
         k_iota_vals<<<grid_for(SC, 256), 256, 0, st>>>(SC, C, vals_out);
         FP_HIP(hipGetLastError());
@@ -160,12 +187,13 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
                                                    vals_out, (unsigned)SC, S, offs, offs + 1, 0,
                                                    kbits, st));
         order = vals_out;
+        skeys = keys_out;
     }
     fp_prof_end(c, FP_K_SORT, ev);
 
     // ---- 4-5: placement + cost ----
-    return fp_pipe_launch(c, S, C, N, b->scen_base, order, b, minc == 0xFFFFFFFFu ? 1u : minc, maxc,
-                          minm == 0xFFFFFFFFu ? 1u : minm, maxm);
+    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, mbits, cmax, mmax, b,
+                          minc == 0xFFFFFFFFu ? 1u : minc, maxc, minm == 0xFFFFFFFFu ? 1u : minm, maxm);
 }
 
 extern "C" int fp_dev_argmin_cost(fp_ctx *c, const uint64_t *cost, uint32_t n, uint32_t *best) {
