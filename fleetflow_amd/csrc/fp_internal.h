@@ -67,7 +67,7 @@ int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *
                             uint32_t *first, uint32_t *count, uint64_t *bitmap);
 
 // tile-pipeline FFD (fp_pipe.hip)
-bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out);
+bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out);
 size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N);
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const uint64_t *skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax, const fp_batch *b,

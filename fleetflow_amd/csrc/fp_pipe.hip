@@ -636,23 +636,30 @@ static void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
 // than ~4 segments adds link latency to the FFD chain.
 constexpr uint32_t MAX_SEG_GROUPS = 40;
 constexpr size_t LDS_HALF_CU = 80 * 1024;
+constexpr uint64_t kNarrowWaves = 1024;  // S x groups at or below which stages hold one group
 
-bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out) {
+bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out) {
     const uint32_t NG = (N + 63) / 64;
     const size_t cap = 160 * 1024;
     if (NG == 0) {
         *G_out = 1; *W_out = 1; *B_out = 1; *lds_out = lds_bytes(1, 1, 2);
         return true;
     }
-    // FLEETPLACE_PIPE_W: force the stage count (tuning experiments only)
-    static const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
-    // FLEETPLACE_PIPE_SEG: groups per segment (tuning experiments only)
-    static const int forced_seg = getenv("FLEETPLACE_PIPE_SEG") ? atoi(getenv("FLEETPLACE_PIPE_SEG")) : 0;
-    const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg : MAX_SEG_GROUPS;
+    // FLEETPLACE_PIPE_W: force the stage count (tuning experiments and tests)
+    const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
+    // FLEETPLACE_PIPE_SEG: groups per segment (tuning experiments and tests)
+    const int forced_seg = getenv("FLEETPLACE_PIPE_SEG") ? atoi(getenv("FLEETPLACE_PIPE_SEG")) : 0;
+    // Few scenarios on a small table leave the GPU idle: one group (64 nodes) per
+    // stage then shortens each check (no register indexing) -- config 2 (1 x 10k x
+    // 1k): 2.39 ms vs 3.02 ms with 10-group stages.  Many scenarios keep 10-group
+    // stages: stages of 1-5 groups put more waves on a CU than it can issue.
+    const bool narrow = (uint64_t)S * NG <= kNarrowWaves;
+    const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg
+                                : narrow ? 4u : MAX_SEG_GROUPS;
     const uint32_t B = (NG + seg_groups - 1) / seg_groups;
     const uint32_t per_seg = (NG + B - 1) / B;
-    for (uint32_t W : {4u, 8u, 2u, 1u, 12u, 16u}) {
-        if (forced_w > 0 && W != (uint32_t)forced_w) continue;
+    // a forced stage count is tried first; sizes it cannot serve fall back to the list
+    for (uint32_t W : {forced_w > 0 ? (uint32_t)forced_w : 4u, 4u, 8u, 2u, 1u, 12u, 16u}) {
         if (W > per_seg && W > 1) continue;
         const uint32_t G = (per_seg + W - 1) / W;
         if (G > MAX_G) continue;
@@ -669,7 +676,7 @@ bool fp_pipe_plan(uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out,
 size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
     uint32_t G, W, B;
     size_t lds;
-    if (!fp_pipe_plan(N, &G, &W, &B, &lds)) return 0;
+    if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return 0;
     const size_t SC = (size_t)S * C, nlinks = (size_t)S * (B - 1), slots = (C + 63) / 64 + 2;
     return 5 * SC * 4 + 256 + nlinks * 128 + (size_t)S * B * 8 + 8 + nlinks * slots * 6 * 64 * 4 + 8 * 256;
 }
@@ -679,7 +686,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
                    uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
     uint32_t G, W, B;
     size_t lds;
-    if (!fp_pipe_plan(N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
+    if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
     if (C >= 0x80000000u) return FP_EOVERFLOW;
     if ((uint64_t)S * B > 0xFFFFFFFFull) return FP_EOVERFLOW;
     // deepest ring (2..4 slots) that keeps two workgroups per CU (else one)

@@ -312,10 +312,40 @@ def test_feasibility_random_vs_oracle(C, N, planner, O):
     assert np.array_equal(first, ef) and np.array_equal(count, ec) and np.array_equal(bm, eb)
 
 
-# ---- pipeline geometry edges: 40 groups (2560 nodes) per segment, 10 per stage ----------
+# ---- pipeline geometry: "wide" (segments of 40 groups, stages of 10) is what many
+# scenarios get, "narrow" (segments of 4, stages of 1 group) what a few small ones get;
+# both are forced here so every size runs through both ------------------------------
+GEOMETRIES = {"wide": ("4", "40"), "narrow": ("4", "4"), "one-stage": ("1", "16")}
+
+
+@pytest.fixture(params=sorted(GEOMETRIES))
+def geometry(request, monkeypatch):
+    w, seg = GEOMETRIES[request.param]
+    monkeypatch.setenv("FLEETPLACE_PIPE_W", w)
+    monkeypatch.setenv("FLEETPLACE_PIPE_SEG", seg)
+    return request.param
+
+
 @pytest.mark.parametrize("C,N,flags", [(4000, 640, 7), (4000, 641, 7), (7000, 2560, 7), (7000, 2561, 7),
-                                       (5000, 5120, 7), (3000, 5121, 3)])
-def test_ffd_geometry_edges(C, N, flags, planner, O):
-    """Stage (640 nodes), segment (2560) and two-segment (5120) boundaries."""
+                                       (5000, 5120, 7), (3000, 5121, 3), (64, 64, 7), (1000, 100, 7)])
+def test_ffd_geometry_edges(C, N, flags, planner, O, geometry):
+    """Stage (64 / 640 nodes), segment (256 / 2560) and two-segment (5120) boundaries."""
     cont, nodes = O.gen_scenario(SEED + 13 * C + N, 3, C, N, flags)
     _check_ffd(planner, O, cont, nodes)
+
+
+def test_ffd_batch_geometries(planner, O, geometry):
+    S, C, N, base = 5, 3000, 1500, 7
+    conts, nodes = [], []
+    for s in range(S):
+        c, n = O.gen_scenario(SEED + 21, base + s, C, N, 7)
+        conts.append(c)
+        nodes.append(n)
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    assign, reason, cost, after = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
+                                                      [cat(nodes, i) for i in range(5)], scen_base=base)
+    for s in range(S):
+        ea, er, eafter, _ = O.place(conts[s], nodes[s])
+        assert np.array_equal(assign[s * C:(s + 1) * C], ea)
+        assert np.array_equal(reason[s * C:(s + 1) * C], er)
+        assert int(cost[s]) == O.cost(ea, N, base + s)
