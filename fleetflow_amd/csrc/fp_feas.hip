@@ -10,7 +10,8 @@
 
 namespace {
 
-constexpr int kBlock = 256;   // containers per block (4 waves)
+constexpr int kBlock = 256;   // threads per block (4 waves)
+constexpr int kPer = 4;       // containers per thread: one LDS node read serves 4 x 64 containers (8: slower)
 constexpr int kTile = 1024;   // nodes per LDS chunk
 
 struct alignas(16) NodeRec {
@@ -27,21 +28,31 @@ struct FeasArgs {
     int split;
 };
 
+// Block = 256 threads x kPer containers: container c = blockIdx.x * 1024 + k * 256 + threadIdx.x,
+// so each of a wave's kPer container words is one bitmap row.
 __global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
     __shared__ NodeRec rec[kTile];
     __shared__ uint32_t sch[kTile];
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wword = (blockIdx.x * kBlock + (threadIdx.x & ~63u)) / 64;  // container word
-    const bool cin = c < a.C;
-    const uint32_t cpu = cin ? a.cpu[c] : 0xFFFFFFFFu;
-    const uint32_t mem = cin ? a.mem[c] : 0xFFFFFFFFu;
-    const uint32_t req = cin ? a.req[c] : 0u;
-    const uint32_t conf = cin ? a.conf[c] : 0u;
+    uint32_t cpu[kPer], mem[kPer], req[kPer], conf[kPer], first[kPer], cnt[kPer], cidx[kPer];
+    uint64_t word[kPer];
+    bool cin[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t c = blockIdx.x * (kBlock * kPer) + k * kBlock + threadIdx.x;
+        cidx[k] = c;
+        cin[k] = c < a.C;
+        // absent lanes get an impossible demand (never fits: cpu > any free cpu)
+        cpu[k] = cin[k] ? a.cpu[c] : 0xFFFFFFFFu;
+        mem[k] = cin[k] ? a.mem[c] : 0xFFFFFFFFu;
+        req[k] = cin[k] ? a.req[c] : 0u;
+        conf[k] = cin[k] ? a.conf[c] : 0u;
+        first[k] = FP_NONE;
+        cnt[k] = 0;
+        word[k] = 0;
+    }
     const uint32_t y0 = blockIdx.y * a.node_span;
     const uint32_t y1 = min(a.N, y0 + a.node_span);
-    uint32_t first = FP_NONE, cnt = 0;
-    uint64_t word = 0;
     for (uint32_t n0 = y0; n0 < y1; n0 += kTile) {
         const uint32_t len = min((uint32_t)kTile, y1 - n0);
         for (uint32_t i = threadIdx.x; i < len; i += kBlock) {
@@ -53,27 +64,39 @@ __global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
         __syncthreads();
         for (uint32_t i = 0; i < len; ++i) {
             const NodeRec r = rec[i];
-            const bool ok = cin && sch[i] && fpd::fits(cpu, mem, req, conf, r.cf, r.mf, r.lab, r.cu);
-            cnt += ok ? 1u : 0u;
-            if (ok && first == FP_NONE) first = n0 + i;
-            if (a.bitmap) {
-                const uint64_t m = __ballot(ok);
-                if (lane == (i & 63)) word = m;
-                if ((i & 63) == 63 || i + 1 == len) {
-                    const uint32_t nb = n0 + (i & ~63u);
-                    if (lane <= (i & 63) && wword < a.WC) a.bitmap[(size_t)wword * a.N + nb + lane] = word;
+            const bool sc = sch[i] != 0u;
+            const uint32_t n = n0 + i;
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                const bool ok = sc & cin[k] & fpd::fits(cpu[k], mem[k], req[k], conf[k], r.cf, r.mf, r.lab, r.cu);
+                cnt[k] += ok ? 1u : 0u;
+                first[k] = min(first[k], ok ? n : FP_NONE);
+                if (a.bitmap) {
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+                    word[k] = lane == (i & 63) ? m : word[k];
+                }
+            }
+            if (a.bitmap && ((i & 63) == 63 || i + 1 == len)) {
+                const uint32_t nb = n0 + (i & ~63u);
+#pragma unroll
+                for (int k = 0; k < kPer; ++k) {
+                    const uint32_t wword = (blockIdx.x * (kBlock * kPer) + k * kBlock + (threadIdx.x & ~63u)) / 64;
+                    if (lane <= (i & 63) && wword < a.WC) a.bitmap[(size_t)wword * a.N + nb + lane] = word[k];
                 }
             }
         }
         __syncthreads();
     }
-    if (!cin) return;
-    if (a.split) {
-        if (first != FP_NONE) atomicMin(&a.first[c], first);
-        if (cnt) atomicAdd(&a.count[c], cnt);
-    } else {
-        a.first[c] = first;
-        a.count[c] = cnt;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (!cin[k]) continue;
+        if (a.split) {
+            if (first[k] != FP_NONE) atomicMin(&a.first[cidx[k]], first[k]);
+            if (cnt[k]) atomicAdd(&a.count[cidx[k]], cnt[k]);
+        } else {
+            a.first[cidx[k]] = first[k];
+            a.count[cidx[k]] = cnt[k];
+        }
     }
 }
 
@@ -89,10 +112,10 @@ int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *
         return FP_EINVAL;
     hipStream_t st = c->stream;
     FP_HIP(hipMemsetAsync(c->d_err, 0, 4, st));
-    const uint32_t xb = (C + kBlock - 1) / kBlock;
+    const uint32_t xb = (C + kBlock * kPer - 1) / (kBlock * kPer);
     // split the node range over blockIdx.y until the grid is >= ~2048 blocks
     uint32_t ysplit = 1;
-    const uint32_t max_split = N ? (N + kTile - 1) / kTile : 1;
+    const uint32_t max_split = N ? (N + 63) / 64 : 1;  // node ranges of >= 64 nodes
     while ((uint64_t)xb * ysplit < 2048 && ysplit < max_split) ysplit *= 2;
     if (ysplit > max_split) ysplit = max_split;
     uint32_t span = N ? (N + ysplit - 1) / ysplit : 0;

@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 from fleetflow_amd import DevBatch, Planner  # noqa: E402
-from fleetflow_amd._lib import FP_K_LEVEL, FP_K_PLACE, FP_K_SORT  # noqa: E402
+from fleetflow_amd._lib import FP_K_FEAS, FP_K_LEVEL, FP_K_PLACE, FP_K_SORT  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (checker / CPU baseline only)
 
 SEED = 0x5EED0000
@@ -124,11 +124,43 @@ def levelize_config(p, dev, reps, cpu):
     return out, el
 
 
+def feas_config(p, dev, name, seed, C, N, reps, cpu, bitmap):
+    """Stage-2 sweep (fp_dev_feasibility) on the pristine node table of a config."""
+    cont, nodes = O.gen_scenario(seed, 0, C, N, 7)
+    db = dev_batch_from(cont, nodes, dev)
+    first_t = torch.empty(C, dtype=torch.int32, device=dev)
+    count_t = torch.empty(C, dtype=torch.int32, device=dev)
+    bm_t = torch.empty(((C + 63) // 64) * N, dtype=torch.int64, device=dev) if bitmap else None
+    p.profile(False)
+    p.profile(True)
+    walls = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        p.dev_feasibility(db, first_t, count_t, bm_t)
+        p.sync()
+        walls.append(time.perf_counter() - t0)
+    k_ms, k_n = p.kernel_stats(FP_K_FEAS)
+    kern_ms = k_ms / max(k_n, 1)
+    out = {"config": name, "C": C, "N": N, "bitmap": bitmap, "gpu_wall_ms": min(walls) * 1e3, "feas_kernel_ms": kern_ms,
+           "evals_per_s": C * N / (kern_ms / 1e3), "work_equiv_GBps": 16 * C * N / (kern_ms / 1e3) / 1e9,
+           "bitmap_GBps": (((C + 63) // 64) * N * 8 / (kern_ms / 1e3) / 1e9) if bitmap else 0.0}
+    if cpu:
+        # checker on a sample of containers (the full C x N sweep is minutes of CPU time)
+        k = min(C, 2000)
+        sub = tuple(np.asarray(a)[:k] for a in cont)
+        (ef, ec, _), cpu_ms = cpu_time(lambda: O.feasibility(sub, nodes, want_bitmap=False))
+        ok = (np.array_equal(first_t[:k].cpu().numpy().view(np.uint32), ef) and
+              np.array_equal(count_t[:k].cpu().numpy().view(np.uint32), ec))
+        out.update({"bit_exact_sample": bool(ok), "cpu_oracle_evals_per_s": k * N / (cpu_ms / 1e3), "cpu_cores": 1})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--only", default="2,3,5")
+    ap.add_argument("--only", default="2,3,5,f")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -147,6 +179,13 @@ def main():
             print(json.dumps(ffd_config(p, dev, "5b: place the DAG's 1M containers on 100k nodes (CYCLE skipped)",
                                         SEED + 5, level.size, 100_000, 7, args.reps, cpu, level=level)),
                   flush=True)
+        if "f" in only:
+            print(json.dumps(feas_config(p, dev, "stage 2 sweep, config-2 shape", SEED + 2, 10_000, 1_000,
+                                         args.reps, cpu, True)), flush=True)
+            print(json.dumps(feas_config(p, dev, "stage 2 sweep, config-3 shape (no bitmap)", SEED + 3,
+                                         1_000_000, 100_000, args.reps, cpu, False)), flush=True)
+            print(json.dumps(feas_config(p, dev, "stage 2 sweep, 250k x 100k with bitmap", SEED + 3,
+                                         250_000, 100_000, args.reps, cpu, True)), flush=True)
 
 
 if __name__ == "__main__":
