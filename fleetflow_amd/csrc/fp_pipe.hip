@@ -36,7 +36,7 @@ __device__ unsigned long long g_pipe_stats[16 * 16];
 #define STAT_ON 1
 // per-batch timeline of scenario 0: [stage][batch] = (t_in_ready, t_prescan, t_cand, t_out_done)
 constexpr int TL_B = 2048;
-__device__ unsigned long long g_pipe_tl[16 * TL_B * 4];
+__device__ unsigned long long g_pipe_tl[16 * TL_B * 8];
 #else
 #define STAT_ADD(w, i, v) ((void)0)
 #define STAT_CLK() 0ull
@@ -127,7 +127,8 @@ __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_
 }
 
 // lane `t` of `old` replaced by the wave-uniform `val` (v_cmp + v_cndmask)
-#define WRITELANE(val, t, old) ((lane == (t)) ? (uint32_t)(val) : (old))
+// v_writelane_b32 (no clang builtin for it in this toolchain; the LLVM intrinsic by name)
+extern "C" __device__ int fp_writelane(int val, int lane_sel, int old) __asm("llvm.amdgcn.writelane.i32");
 
 // bucket index: largest k with T[k] <= v (T ascending, T[0] = 0; lane base + k holds
 // T[k]).  Binary search through ds_bpermute: no scalar registers held across the
@@ -183,18 +184,32 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     const uint32_t my_t = lane < (uint32_t)K ? a.tc[lane] : a.tm[lane - K];
     const uint32_t gbase = (b * W + w) * G;             // first (global) group of this tile
     uint64_t *Mw = M + (size_t)w * G * K * 2;           // the tile's masks
-    uint32_t rcf[G], rmf[G], rcu[G], rlab[G];           // the tile's node records
+    // The tile's node records.  Unschedulable (and padding) nodes are stored so that every
+    // container with a nonzero field fails the exact check on them: cpu = mem = 0, all
+    // conflict bits used, all (inverted) label bits missing.  The all-zero container, which
+    // would pass, never reaches the check (placed on the tile's first schedulable node).
+    // rlab holds ~labels: label and conflict tests become one ((~lab & req) | (cu & conf)) == 0.
+    uint32_t rcf[G], rmf[G], rcu[G], rlab[G];
     uint32_t schedbits = 0, usedbits = 0;               // bit g for node (g, lane)
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t n = (gbase + g) * 64 + lane;
         const bool in = n < N;
         const bool sc = in && a.sched[nb + n] != 0;
-        rcf[g] = in ? a.cf[nb + n] : 0u;
-        rmf[g] = in ? a.mf[nb + n] : 0u;
-        rcu[g] = in ? a.cu[nb + n] : 0u;
-        rlab[g] = in ? a.lab[nb + n] : 0u;
+        rcf[g] = sc ? a.cf[nb + n] : 0u;
+        rmf[g] = sc ? a.mf[nb + n] : 0u;
+        rcu[g] = sc ? a.cu[nb + n] : 0xFFFFFFFFu;
+        rlab[g] = sc ? ~a.lab[nb + n] : 0xFFFFFFFFu;
         schedbits |= sc ? (1u << g) : 0u;
+    }
+    uint32_t zs_g = G, zs_l = 0;  // the tile's first schedulable node (all-zero containers)
+#pragma unroll
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint64_t sm = __builtin_amdgcn_ballot_w64(((schedbits >> g) & 1u) != 0u);
+        if (zs_g == G && sm) {
+            zs_g = g;
+            zs_l = (uint32_t)__builtin_ctzll(sm);
+        }
     }
     for (uint32_t g = 0; g < G; ++g) {
         const bool sc = (schedbits >> g) & 1u;
@@ -354,7 +369,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             const uint64_t *mg = Mw + (size_t)g * K * 2;
             if (valid && (mg[kc * 2] & mg[km * 2 + 1] & e)) cand |= 1u << g;
         }
-        uint64_t todo = __builtin_amdgcn_ballot_w64(cand != 0);
+        const bool zero = valid && (cpu | mem | req | conf) == 0u;
+        uint64_t todo = __builtin_amdgcn_ballot_w64(cand != 0 && !zero);
         uint64_t placed = 0;
         uint32_t my_assign = FP_NONE;
         if (STAT_ON) {
@@ -364,6 +380,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         ck_b = STAT_CLK(); ck_pre += ck_b - ck_a; ck_a = ck_b;
 #ifdef FP_PIPE_STATS
         const unsigned long long tl_pre = ck_b;
+        const uint32_t tl_checks0 = st_checks, tl_hits0 = st_hits, tl_todo = (uint32_t)__popcll(todo);
 #endif
         // Exact first fit, container by container in FFD order; group g's records are
         // read and written in registers through a wave-uniform index.
@@ -375,43 +392,63 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                 const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
                 const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
                 const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
-                uint32_t cc = __builtin_amdgcn_readlane(cand, ti);
-                while (cc) {
-                    const uint32_t g = (uint32_t)__builtin_ctz(cc);
+                uint32_t cc = __builtin_amdgcn_readlane(cand, ti);  // != 0 for a todo container
+                uint32_t g, x, y, z;
+                uint64_t m, done;
+                // one exit (a match, or no candidate left): a loop with a second exit for
+                // the match gets a merged flag and eight more scalar ops per check
+                do {
+                    g = (uint32_t)__builtin_ctz(cc);
                     cc &= cc - 1;
-                    const uint32_t x = rcf[g], y = rmf[g], z = rcu[g], lb = rlab[g];
+                    x = rcf[g]; y = rmf[g]; z = rcu[g];
+                    const uint32_t lb = rlab[g];
                     if (STAT_ON) st_checks++;
                     // one v_cmp per condition straight into a scalar mask, ANDed on the
                     // SALU (a single ballot of the combined bool costs two extra
                     // dependent VALU ops on the chain)
-                    const uint64_t m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
-                                       __builtin_amdgcn_ballot_w64((lb & c_req) == c_req) &
-                                       __builtin_amdgcn_ballot_w64((z & c_conf) == 0u) &
-                                       __builtin_amdgcn_ballot_w64(((schedbits >> g) & 1u) != 0u);
-                    if (m) {
-                        // placement, branch-free: lane l's record changes; one all-lane
-                        // ds_and_b64 clears the crossed buckets (lanes 0-31 cpu masks,
-                        // lanes 32-63 mem masks of group g)
-                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                        const uint32_t oc = __builtin_amdgcn_readlane(x, l);
-                        const uint32_t om = __builtin_amdgcn_readlane(y, l);
-                        const uint32_t nc = oc - c_cpu, nm = om - c_mem;
-                        const bool me = lane == l;
-                        rcf[g] = me ? nc : x;
-                        rmf[g] = me ? nm : y;
-                        rcu[g] = me ? (z | c_conf) : z;
-                        const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
-                        const bool crossed = (my_t <= ov) & (my_t > nv);
-                        atomicAnd((unsigned long long *)&Mw[(size_t)g * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
-                                  crossed ? ~(1ull << l) : ~0ull);
-                        n_used += ((__builtin_amdgcn_readlane(usedbits, l) >> g) & 1u) ^ 1u;
-                        usedbits |= me ? (1u << g) : 0u;
-                        placed |= 1ull << ti;
-                        my_assign = WRITELANE((gbase + g) * 64 + l, ti, my_assign);
-                        if (STAT_ON) st_hits++;
-                        break;
-                    }
+                    m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
+                        __builtin_amdgcn_ballot_w64(((lb & c_req) | (z & c_conf)) == 0u);
+                    // exit flag = m | (cc == 0), kept on the SALU (the compiler moves the 64-bit
+                    // test to the VALU otherwise)
+                    asm("s_cmp_eq_u32 %1, 0\n\ts_cselect_b64 %0, 1, 0\n\ts_or_b64 %0, %0, %2"
+                        : "=&s"(done) : "s"(cc), "s"(m) : "scc");
+                } while (done == 0u);
+                if (m) {
+                    // placement, branch-free: lane l's record changes; one all-lane
+                    // ds_and_b64 clears the crossed buckets (lanes 0-31 cpu masks,
+                    // lanes 32-63 mem masks of group g)
+                    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                    const uint32_t oc = __builtin_amdgcn_readlane(x, l);
+                    const uint32_t om = __builtin_amdgcn_readlane(y, l);
+                    const uint32_t nc = oc - c_cpu, nm = om - c_mem;
+                    const uint32_t ux = (uint32_t)fp_writelane((int)nc, (int)l, (int)x);
+                    const uint32_t uy = (uint32_t)fp_writelane((int)nm, (int)l, (int)y);
+                    const uint32_t uz = (uint32_t)fp_writelane((int)(__builtin_amdgcn_readlane(z, l) | c_conf), (int)l, (int)z);
+                    // keep the three indexed writes adjacent: one s_set_gpr_idx window
+                    __builtin_amdgcn_sched_barrier(0);
+                    rcf[g] = ux;
+                    rmf[g] = uy;
+                    rcu[g] = uz;
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
+                    const bool crossed = (my_t <= ov) & (my_t > nv);
+                    atomicAnd((unsigned long long *)&Mw[(size_t)g * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
+                              crossed ? ~(1ull << l) : ~0ull);
+                    usedbits = (uint32_t)fp_writelane(
+                        (int)(__builtin_amdgcn_readlane(usedbits, l) | (1u << g)), (int)l, (int)usedbits);
+                    placed |= 1ull << ti;
+                    my_assign = (uint32_t)fp_writelane((int)((gbase + g) * 64 + l), (int)ti, (int)my_assign);
+                    if (STAT_ON) st_hits++;
                 }
+            }
+        }
+        if (zs_g < G) {
+            // all-zero containers change no record: each takes the first schedulable node
+            const uint64_t zm = __builtin_amdgcn_ballot_w64(zero);
+            if (zm) {
+                placed |= zm;
+                my_assign = zero ? (gbase + zs_g) * 64 + zs_l : my_assign;
+                usedbits |= lane == zs_l ? (1u << zs_g) : 0u;
             }
         }
         ck_b = STAT_CLK(); ck_cand += ck_b - ck_a; ck_a = ck_b;
@@ -425,8 +462,10 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         }
 #ifdef FP_PIPE_STATS
         if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B) {
-            unsigned long long *tl = &g_pipe_tl[((size_t)w * TL_B + tl_idx) * 4];
+            // global stage b * W + w; per batch: ready, prescan end, loop end, checks, hits, todo
+            unsigned long long *tl = &g_pipe_tl[((size_t)(b * W + w) * TL_B + tl_idx) * 8];
             tl[0] = ck_t0_batch; tl[1] = tl_pre; tl[2] = tl_cand;
+            tl[3] = st_checks - tl_checks0; tl[4] = st_hits - tl_hits0; tl[5] = tl_todo;
         }
 #endif
         const bool fwd = valid && !((placed >> lane) & 1ull);
@@ -519,6 +558,12 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             lds_rel(&octl[0], ohead);
         }
     }
+    {  // nodes of this stage that received a container
+        uint32_t u = (uint32_t)__popc(usedbits);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) u += (uint32_t)__shfl_xor((int)u, o);
+        n_used = u;
+    }
     if (lane == 0) {
         atomicAdd(&CNT[0], n_used);
         atomicAdd(&CNT[1], n_rej);
@@ -533,7 +578,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t n = (gbase + g) * 64 + lane;
-        if (n < N) {
+        if (n < N && ((schedbits >> g) & 1u)) {  // unschedulable records were never loaded
             a.cf[nb + n] = rcf[g];
             a.mf[nb + n] = rmf[g];
             a.cu[nb + n] = rcu[g];
@@ -745,7 +790,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
 
 #ifdef FP_PIPE_STATS
 extern "C" int fp_debug_pipe_timeline(unsigned long long *out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_tl), sizeof(unsigned long long) * 16 * TL_B * 4) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_tl), sizeof(unsigned long long) * 16 * TL_B * 8) != hipSuccess)
         return FP_EDEVICE;
     return FP_OK;
 }

@@ -349,3 +349,30 @@ def test_ffd_batch_geometries(planner, O, geometry):
         assert np.array_equal(assign[s * C:(s + 1) * C], ea)
         assert np.array_equal(reason[s * C:(s + 1) * C], er)
         assert int(cost[s]) == O.cost(ea, N, base + s)
+
+
+@pytest.mark.parametrize("N", [700, 3000])
+def test_ffd_zero_demand_mixed(N, planner, O, geometry):
+    """All-zero containers among ordinary ones; the first tiles (and scattered nodes) are
+    unschedulable, so zero containers must skip whole stages; some containers use only labels
+    or only conflicts with zero cpu/mem."""
+    rng = np.random.default_rng(N)
+    C = 5000
+    cont, nodes = O.gen_scenario(SEED + 77, 1, C, N, 7)
+    cpu, mem, req, conf = (np.array(a, np.uint32) for a in cont)
+    z = rng.random(C) < 0.05          # all-zero
+    cpu[z] = mem[z] = req[z] = conf[z] = 0
+    lab_only = (~z) & (rng.random(C) < 0.03)
+    cpu[lab_only] = mem[lab_only] = 0
+    conf[lab_only] = 0
+    conf_only = (~z) & (~lab_only) & (rng.random(C) < 0.03)
+    cpu[conf_only] = mem[conf_only] = 0
+    req[conf_only] = 0
+    conf[conf_only] = (1 << rng.integers(0, 32, int(conf_only.sum()))).astype(np.uint32)
+    cf, mf, lab, cu, sc = (np.array(a) for a in nodes)
+    sc = sc.astype(np.uint8)
+    sc[:650] = 0                      # whole first stage (and part of the second) cordoned
+    sc[rng.random(N) < 0.1] = 0
+    _check_ffd(planner, O, (cpu, mem, req, conf), (cf, mf, lab, cu, sc))
+    # nothing schedulable at all: zero containers are NOFIT too
+    _check_ffd(planner, O, (cpu[:300], mem[:300], req[:300], conf[:300]), (cf, mf, lab, cu, np.zeros(N, np.uint8)))

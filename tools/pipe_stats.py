@@ -61,20 +61,20 @@ def main():
 
 
 def timeline(out_path):
-    """Dump scenario 0's per-batch timeline (stats build) to out_path as CSV."""
+    """Dump scenario 0's per-batch timeline (stats build) to out_path as CSV (global stage = segment * W + stage)."""
     L = _lib.load()
     f = L.fp_debug_pipe_timeline
     f.argtypes = [ct.POINTER(ct.c_ulonglong)]
     TLB = 2048
-    buf = (ct.c_ulonglong * (16 * TLB * 4))()
+    buf = (ct.c_ulonglong * (16 * TLB * 8))()
     f(buf)
     with open(out_path, "w") as fo:
-        fo.write("stage,batch,t_ready,t_prescan,t_cand\n")
+        fo.write("stage,batch,t_ready,t_prescan,t_cand,checks,hits,todo\n")
         for w in range(16):
             for b in range(TLB):
-                v = [buf[(w * TLB + b) * 4 + i] for i in range(3)]
+                v = [buf[(w * TLB + b) * 8 + i] for i in range(6)]
                 if v[0]:
-                    fo.write(f"{w},{b},{v[0]},{v[1]},{v[2]}\n")
+                    fo.write(f"{w},{b}," + ",".join(str(x) for x in v) + "\n")
 
 
 if __name__ == "__main__":
