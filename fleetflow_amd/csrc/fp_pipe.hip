@@ -54,10 +54,6 @@ constexpr uint32_t CYC = 0x80000000u;
 constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s
 constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per group)
 constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
-#ifndef FP_SB
-#define FP_SB 64
-#endif
-constexpr int SB = FP_SB;           // containers per corner sub-batch
 
 struct PipeArgs {
     uint32_t C, N, scen_base, W, G, R;
@@ -141,6 +137,18 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t my_t, int bas
         k += t <= v ? step : 0u;
     }
     return k;
+}
+
+// min over the wave's 64 lanes, broadcast (DPP row shifts + row broadcasts into lane 63;
+// lanes without a DPP source read UINT32_MAX, the identity of min)
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 // Node records (cpu_free, mem_free, conflict_used, labels) of a wave's tile live
@@ -334,41 +342,24 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         // Lane-parallel candidate groups, a superset of the feasible groups (masks
         // only lose bits).  Two filters are ANDed:
         //  * per-container bucket masks B_cpu[g][kc] & B_mem[g][km];
-        //  * an exact 2-D "corner" mask per sub-batch q of SB consecutive containers:
-        //    E_q[g] = {l : sched && cpu_free >= min cpu(q) && mem_free >= min mem(q)}.
+        //  * an exact 2-D "corner" mask of the batch:
+        //    E[g] = {l : cpu_free >= min cpu && mem_free >= min mem} (unschedulable
+        //    records are zero, so they drop out unless a demand is zero).
         //    FFD order makes a batch's cpu range narrow, so the corner is tight in
-        //    cpu.  SB = 64 (one corner per batch, one ballot per group) ran the
-        //    config-4 bench 12% faster than SB = 8 (1.64 vs 1.96 checks per
-        //    container, but an 8x cheaper prescan on every stage a container visits).
-        const uint32_t vc = valid ? cpu : 0xFFFFFFFFu, vm = valid ? mem : 0xFFFFFFFFu;
-        uint32_t qc = vc, qm = vm;  // min over the lane's sub-batch (xor butterfly)
-#pragma unroll
-        for (int o = 1; o < SB; o <<= 1) {
-            qc = min(qc, (uint32_t)__shfl_xor((int)qc, o));
-            qm = min(qm, (uint32_t)__shfl_xor((int)qm, o));
-        }
+        //    cpu.  One corner per 64-container batch ran the config-4 bench 12% faster
+        //    than one per 8 containers (1.64 vs 1.96 checks per container, but an 8x
+        //    cheaper prescan on every stage a container visits).
+        const uint32_t qc = wave_min(valid ? cpu : 0xFFFFFFFFu), qm = wave_min(valid ? mem : 0xFFFFFFFFu);
+        // every mask load is issued before the first use (no per-group LDS round trip)
+        const uint32_t oc = kc * 2, om = km * 2 + 1;
         uint32_t cand = 0;
-        const uint32_t my_q = lane / SB;
-        // the 64/SB corners, broadcast into VGPRs (readlane-to-SGPR copies of them get
-        // hoisted out of the loops and spill scalar registers)
-        uint32_t cqv[64 / SB], mqv[64 / SB];
-#pragma unroll
-        for (uint32_t q = 0; q < 64 / SB; ++q) {
-            cqv[q] = (uint32_t)__shfl((int)qc, (int)(q * SB));
-            mqv[q] = (uint32_t)__shfl((int)qm, (int)(q * SB));
-        }
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
-            const bool sc = (schedbits >> g) & 1u;
-            uint64_t e = 0;  // E_{my_q}[g]
-#pragma unroll
-            for (uint32_t q = 0; q < 64 / SB; ++q) {
-                const uint64_t eq = __builtin_amdgcn_ballot_w64(sc & (rcf[g] >= cqv[q]) & (rmf[g] >= mqv[q]));
-                e = my_q == q ? eq : e;
-            }
+            const uint64_t e = __builtin_amdgcn_ballot_w64((rcf[g] >= qc) & (rmf[g] >= qm));
             const uint64_t *mg = Mw + (size_t)g * K * 2;
-            if (valid && (mg[kc * 2] & mg[km * 2 + 1] & e)) cand |= 1u << g;
+            cand |= (mg[oc] & mg[om] & e) ? 1u << g : 0u;
         }
+        cand = valid ? cand : 0u;
         const bool zero = valid && (cpu | mem | req | conf) == 0u;
         uint64_t todo = __builtin_amdgcn_ballot_w64(cand != 0 && !zero);
         uint64_t placed = 0;
