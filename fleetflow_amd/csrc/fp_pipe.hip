@@ -23,7 +23,14 @@
 // clearing bits on placement and a stale mask is always a superset: only
 // candidate groups get the exact check.
 #include "fp_internal.h"
+// 10-group stages (the wide geometry: configs 3, 4, 5) run the hand-scheduled candidate
+// loop of fp_pipe_asm.h; -DFP_NO_ASM builds the C++ loop everywhere (A/B, reference)
+#ifndef FP_NO_ASM
+#define FP_ASM
+#endif
+#include "fp_pipe_asm.h"
 #include <stdlib.h>
+#include <type_traits>
 
 #ifdef FP_PIPE_STATS
 // diagnostics build only: per stage w: [0] visits [1] cand checks [2] hits [3] batches
@@ -161,6 +168,16 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 //   CTL : (W-1)*8 u32 + 8 u32   per link [0]=head [1]=tail [2..2+R)=slot counts; then
 //                               CNT [0]=n_used [1]=n_rej [2]=abort
 //   D   : (W-1)*R*NF*64 u32     ring slots, field-major
+// a tile's records of one kind, one register per group (a plain array: register-
+// promoted, read and written through s_set_gpr_idx; a pinned tuple in the asm build)
+#ifdef FP_ASM
+template <uint32_t G>
+using RecT = typename std::conditional<G == 10, rec10, uint32_t[G]>::type;
+#else
+template <uint32_t G>
+using RecT = uint32_t[G];
+#endif
+
 template <uint32_t G>
 __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -197,7 +214,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     // conflict bits used, all (inverted) label bits missing.  The all-zero container, which
     // would pass, never reaches the check (placed on the tile's first schedulable node).
     // rlab holds ~labels: label and conflict tests become one ((~lab & req) | (cu & conf)) == 0.
-    uint32_t rcf[G], rmf[G], rcu[G], rlab[G];
+    RecT<G> rcf, rmf, rcu, rlab;
     uint32_t schedbits = 0, usedbits = 0;               // bit g for node (g, lane)
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
@@ -372,6 +389,19 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
 #ifdef FP_PIPE_STATS
         const unsigned long long tl_pre = ck_b;
         const uint32_t tl_checks0 = st_checks, tl_hits0 = st_hits, tl_todo = (uint32_t)__popcll(todo);
+#endif
+#ifdef FP_ASM
+        // Exact first fit, container by container in FFD order: the hand-scheduled
+        // loop (fp_pipe_asm.h) for 10-group stages.  Same algorithm as the C++ loop below.
+        if constexpr (G == 10) {
+            const uint32_t lane_sel = lane < 32u ? 0xFFFFFFFFu : 0u;
+            const uint32_t maddr = (uint32_t)(size_t)(__attribute__((address_space(3))) uint64_t *)(
+                Mw + (lane & (K - 1)) * 2 + (lane >> 5));
+            uint32_t nchk = 0, nhit = 0;
+            fpp_asm_batch(todo, placed, my_assign, usedbits, rcf, rmf, rcu, rlab, cpu, mem, req, conf, cand, my_t,
+                          lane_sel, maddr, (gbase * 64u), nchk, nhit);
+            if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
+        } else
 #endif
         // Exact first fit, container by container in FFD order; group g's records are
         // read and written in registers through a wave-uniform index.

@@ -1,0 +1,140 @@
+// Hand-scheduled candidate loop of k_ffd_pipe (one batch, one stage): exact first fit,
+// container by container in FFD order.  Same algorithm and state as the C++ loop in
+// fp_pipe.hip, written as one inline-asm block so that
+//   * a group's four records are read through ONE s_set_gpr_idx window and written back
+//     through one (the records sit in fixed VGPR tuples, v[88:127], pinned by operand
+//     constraints -- the only way to name an indexed base register in inline asm);
+//   * label and conflict become one test: ((~lab & req) | (cu & conf)) == 0;
+//   * the check loop has one scalar exit test per candidate and a single SCC branch on
+//     the match;
+//   * the bucket-mask update is one ds_mskor_b64 with no per-lane select of the old value.
+// gfx950 (GFX9 encoding): one SGPR per VALU op, lane selects come from SALU results or
+// M0, and M0 is reloaded after every s_set_gpr_idx window (the window overwrites it);
+// M0 is restored on exit (the compiler treats it as reserved).  Written for 10-group
+// stages (the wide geometry): records v[88:127], scratch v[76:87], so the wave stays
+// within 128 VGPRs (four workgroups of four waves per CU).
+#pragma once
+#include <stdint.h>
+
+namespace fpp {
+
+typedef uint32_t rec10 __attribute__((ext_vector_type(10)));
+
+#ifdef FP_PIPE_STATS
+#define FPP_ASM_CNT_CHECK "s_add_u32 %[nchk], %[nchk], 1\n\t"
+#define FPP_ASM_CNT_HIT "s_add_u32 %[nhit], %[nhit], 1\n\t"
+#else
+#define FPP_ASM_CNT_CHECK ""
+#define FPP_ASM_CNT_HIT ""
+#endif
+
+// todo: containers (lanes) with candidate groups, cleared as they are processed
+// placed / asg / used: placed-lane mask, per-lane assignment, per-lane used-group bits
+// rcf rmf rcu rlab: the stage's records (cpu_free, mem_free, conflict_used, ~labels)
+// lsel: ~0 on lanes 0-31 (cpu thresholds), 0 on lanes 32-63 (mem thresholds)
+// maddr: LDS byte address of this lane's mask word in group 0 (group stride 512 B)
+__device__ __forceinline__ void fpp_asm_batch(uint64_t &todo, uint64_t &placed, uint32_t &asg, uint32_t &used,
+                                              rec10 &rcf, rec10 &rmf, rec10 &rcu, rec10 &rlab, uint32_t cpu,
+                                              uint32_t mem, uint32_t req, uint32_t conf, uint32_t cand,
+                                              uint32_t my_t, uint32_t lsel, uint32_t maddr, uint32_t gb64,
+                                              uint32_t &nchk, uint32_t &nhit) {
+    uint32_t ti, cc, ccpu, cmem, creq, cconf, g, l, oc, om, m0sv;
+    uint64_t tbit, m, m2;
+    asm volatile(
+        "s_mov_b32 %[m0sv], m0\n\t"
+        "v_mov_b32 v82, 1\n\t"
+        "v_mov_b32 v83, 0\n\t"
+        "v_mov_b32 v84, 0\n\t"
+        "v_mov_b32 v85, 0\n\t"
+        "s_cmp_eq_u64 %[todo], 0\n\t"
+        "s_cbranch_scc1 .Lfpp_end%=\n"
+        ".Lfpp_cont%=:\n\t"
+        "s_ff1_i32_b64 %[ti], %[todo]\n\t"
+        "s_lshl_b64 %[tbit], 1, %[ti]\n\t"
+        "s_andn2_b64 %[todo], %[todo], %[tbit]\n\t"
+        "v_readlane_b32 %[cc], %[cand], %[ti]\n\t"
+        "v_readlane_b32 %[ccpu], %[cpu], %[ti]\n\t"
+        "v_readlane_b32 %[cmem], %[mem], %[ti]\n\t"
+        "v_readlane_b32 %[creq], %[req], %[ti]\n\t"
+        "v_readlane_b32 %[cconf], %[conf], %[ti]\n"
+        ".Lfpp_check%=:\n\t"
+        "s_ff1_i32_b32 %[g], %[cc]\n\t"
+        "s_set_gpr_idx_on %[g], gpr_idx(SRC0)\n\t"
+        "v_mov_b32 v76, v88\n\t"
+        "v_mov_b32 v77, v98\n\t"
+        "v_mov_b32 v78, v108\n\t"
+        "v_mov_b32 v79, v118\n\t"
+        "s_set_gpr_idx_off\n\t"
+        FPP_ASM_CNT_CHECK
+        "s_bitset0_b32 %[cc], %[g]\n\t"
+        "v_cmp_ge_u32_e64 %[m], v76, %[ccpu]\n\t"
+        "v_cmp_ge_u32_e64 %[m2], v77, %[cmem]\n\t"
+        "v_and_b32_e32 v79, %[creq], v79\n\t"
+        "v_and_or_b32 v79, v78, %[cconf], v79\n\t"
+        "s_and_b64 %[m], %[m], %[m2]\n\t"
+        "v_cmp_eq_u32_e64 %[m2], 0, v79\n\t"
+        "s_and_b64 %[m], %[m], %[m2]\n\t"
+        "s_cbranch_scc1 .Lfpp_hit%=\n\t"
+        "s_cmp_lg_u32 %[cc], 0\n\t"
+        "s_cbranch_scc1 .Lfpp_check%=\n\t"
+        "s_branch .Lfpp_next%=\n"
+        ".Lfpp_hit%=:\n\t"
+        FPP_ASM_CNT_HIT
+        "s_ff1_i32_b64 %[l], %[m]\n\t"
+        "v_readlane_b32 %[oc], v76, %[l]\n\t"
+        "v_readlane_b32 %[om], v77, %[l]\n\t"
+        "v_readlane_b32 %[creq], v78, %[l]\n\t"
+        "v_readlane_b32 %[cc], %[used], %[l]\n\t"
+        "s_mov_b32 m0, %[l]\n\t"
+        "s_sub_u32 %[ccpu], %[oc], %[ccpu]\n\t"    // new cpu_free
+        "s_sub_u32 %[cmem], %[om], %[cmem]\n\t"    // new mem_free
+        "s_or_b32 %[creq], %[creq], %[cconf]\n\t"  // new conflict_used
+        "s_bitset1_b32 %[cc], %[g]\n\t"            // node used
+        "v_writelane_b32 v76, %[ccpu], m0\n\t"
+        "v_writelane_b32 v77, %[cmem], m0\n\t"
+        "v_writelane_b32 v78, %[creq], m0\n\t"
+        "v_writelane_b32 %[used], %[cc], m0\n\t"
+        "s_set_gpr_idx_on %[g], gpr_idx(DST)\n\t"
+        "v_mov_b32 v88, v76\n\t"
+        "v_mov_b32 v98, v77\n\t"
+        "v_mov_b32 v108, v78\n\t"
+        "s_set_gpr_idx_off\n\t"
+        // bucket masks (lanes 0-31 cpu, 32-63 mem): clear bit l where T <= old && T > new
+        "v_mov_b32 v86, %[om]\n\t"
+        "v_bfi_b32 v86, %[lsel], %[oc], v86\n\t"
+        "v_mov_b32 v87, %[cmem]\n\t"
+        "v_bfi_b32 v87, %[lsel], %[ccpu], v87\n\t"
+        "v_cmp_le_u32_e64 %[m], %[myt], v86\n\t"
+        "v_cmp_gt_u32_e64 %[m2], %[myt], v87\n\t"
+        "s_and_b64 %[m], %[m], %[m2]\n\t"
+        "v_lshlrev_b64 v[80:81], %[l], v[82:83]\n\t"
+        "v_cndmask_b32_e64 v80, 0, v80, %[m]\n\t"
+        "v_cndmask_b32_e64 v81, 0, v81, %[m]\n\t"
+        "v_lshl_add_u32 v86, %[g], 9, %[maddr]\n\t"
+        "ds_mskor_b64 v86, v[80:81], v[84:85]\n\t"
+        // assignment of lane ti: gb64 + g * 64 + l
+        "s_lshl_b32 %[oc], %[g], 6\n\t"
+        "s_add_u32 %[oc], %[oc], %[gb64]\n\t"
+        "s_or_b32 %[oc], %[oc], %[l]\n\t"
+        "s_mov_b32 m0, %[ti]\n\t"
+        "v_writelane_b32 %[asg], %[oc], m0\n\t"
+        "s_or_b64 %[placed], %[placed], %[tbit]\n"
+        ".Lfpp_next%=:\n\t"
+        "s_cmp_lg_u64 %[todo], 0\n\t"
+        "s_cbranch_scc1 .Lfpp_cont%=\n"
+        ".Lfpp_end%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b32 m0, %[m0sv]"
+        : [todo] "+s"(todo), [placed] "+s"(placed), [asg] "+v"(asg), [used] "+v"(used),
+          [nchk] "+s"(nchk), [nhit] "+s"(nhit), [rcf] "+{v[88:97]}"(rcf), [rmf] "+{v[98:107]}"(rmf),
+          [rcu] "+{v[108:117]}"(rcu), [rlab] "+{v[118:127]}"(rlab), [ti] "=&s"(ti), [cc] "=&s"(cc),
+          [ccpu] "=&s"(ccpu), [cmem] "=&s"(cmem), [creq] "=&s"(creq), [cconf] "=&s"(cconf), [g] "=&s"(g),
+          [l] "=&s"(l), [oc] "=&s"(oc), [om] "=&s"(om), [tbit] "=&s"(tbit), [m] "=&s"(m), [m2] "=&s"(m2),
+          [m0sv] "=&s"(m0sv)
+        : [cand] "v"(cand), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [myt] "v"(my_t),
+          [lsel] "v"(lsel), [maddr] "v"(maddr), [gb64] "s"(gb64)
+        : "scc", "memory", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85",
+          "v86", "v87");
+}
+
+}  // namespace fpp
