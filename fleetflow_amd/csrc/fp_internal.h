@@ -70,7 +70,8 @@ int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *
 bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out);
 size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N);
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
-                   const uint64_t *skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax, const fp_batch *b,
+                   const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
+                   const fp_batch *b,
                    uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm);
 
 // ---- device helpers ----

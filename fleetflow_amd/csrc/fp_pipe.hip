@@ -626,17 +626,18 @@ __global__ void k_cost_reduce(uint32_t S, uint32_t B, uint32_t scen_base, const 
 }
 
 // Sorted SoA for the pipeline.  cpu and mem come back out of the sorted radix keys
-// (key = (cmax - cpu) << mbits | (mmax - mem), coalesced), so only req, conf and
-// level are gathered at random; without keys (all-zero demands) everything is.
+// (key = [scenario] << kbits | (cmax - cpu) << mbits | (mmax - mem), coalesced; the
+// scenario field, if any, is masked off), so only req, conf and level are gathered at
+// random; without keys (all-zero demands) everything is.
+template <class KeyT>
 __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
-                                const uint64_t *__restrict__ skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax,
+                                const KeyT *__restrict__ skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax,
                                 const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
                                 const uint32_t *__restrict__ req, const uint32_t *__restrict__ conf,
                                 const uint32_t *__restrict__ level, uint32_t *__restrict__ s_cpu,
                                 uint32_t *__restrict__ s_mem, uint32_t *__restrict__ s_req,
                                 uint32_t *__restrict__ s_conf, uint32_t *__restrict__ s_idx) {
     const size_t total = (size_t)S * C;
-    const uint64_t mmask = mbits >= 64 ? ~0ull : ((1ull << mbits) - 1ull);
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (size_t)gridDim.x * blockDim.x) {
         const size_t base = i - i % C;
@@ -644,8 +645,8 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
         const size_t src = base + j;
         if (skeys) {
             const uint64_t k = skeys[i];
-            s_cpu[i] = (uint32_t)(cmax - (mbits >= 64 ? 0ull : (k >> mbits)));
-            s_mem[i] = (uint32_t)(mmax - (k & mmask));
+            s_cpu[i] = (uint32_t)(cmax - (mbits >= 64 ? 0ull : ((k >> mbits) & cmax)));
+            s_mem[i] = (uint32_t)(mmax - (k & mmax));
         } else {
             s_cpu[i] = cpu[src];
             s_mem[i] = mem[src];
@@ -748,8 +749,8 @@ size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
 }
 
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
-                   const uint64_t *skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax, const fp_batch *b,
-                   uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
+                   const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
+                   const fp_batch *b, uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
     uint32_t G, W, B;
     size_t lds;
     if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
@@ -778,9 +779,14 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     {
         size_t g = (SC + 255) / 256;
         if (g > 16384) g = 16384;
-        k_gather_sorted<<<(unsigned)g, 256, 0, st>>>(S, C, order, skeys, mbits, cmax, mmax, b->cpu_m, b->mem_mib,
-                                                    b->req_labels, b->conflict,
-                                                    b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
+        if (key_bytes == 4)
+            k_gather_sorted<uint32_t><<<(unsigned)g, 256, 0, st>>>(
+                S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, b->cpu_m, b->mem_mib, b->req_labels,
+                b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
+        else
+            k_gather_sorted<uint64_t><<<(unsigned)g, 256, 0, st>>>(
+                S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, b->cpu_m, b->mem_mib, b->req_labels,
+                b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
         FP_HIP(hipGetLastError());
     }
     PipeArgs a;

@@ -3,13 +3,17 @@
 //
 // Pipeline per fp_dev_place_batch call:
 //   1. k_key_bounds : max(cpu_m), max(mem_mib) over the batch (exact key width)
-//   2. k_make_keys  : key = ((cmax-cpu) << mb) | (mmax-mem), value = container index
-//   3. rocprim segmented radix sort (stable)  => (cpu desc, mem desc, index asc)
+//   2. k_make_keys  : key = (scenario << kb) | ((cmax-cpu) << mb) | (mmax-mem), value =
+//                     container index; u32 keys when the fields fit 32 bits, else u64
+//   3. rocprim device-wide radix sort (stable; the scenario field keeps scenarios
+//      apart) => (cpu desc, mem desc, index asc) per scenario.  Keys wider than 64
+//      bits with the scenario field fall back to the segmented sort.
 //   4. k_ffd_pipe   : (fp_pipe.hip) per scenario, containers in key order stream
 //                     through a pipeline of node-group stages (LDS-resident node
 //                     tiles); lowest feasible node wins, capacity updated in place.
 //   5. k_cost_reduce: packed cost per scenario from the per-segment counters.
 #include "fp_internal.h"
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 namespace {
@@ -66,13 +70,16 @@ __global__ __launch_bounds__(256) void k_key_bounds(const uint32_t *__restrict__
     }
 }
 
+template <class KeyT>
 __global__ void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
-                            size_t n, uint32_t C, uint32_t mb, uint64_t cmax, uint64_t mmax,
-                            uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+                            size_t n, uint32_t C, uint32_t kb, uint32_t mb, uint64_t cmax, uint64_t mmax,
+                            KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
-        keys[i] = ((cmax - cpu[i]) << mb) | (mmax - mem[i]);
-        vals[i] = (uint32_t)(i % C);
+        const uint32_t s = (uint32_t)(i / C), j = (uint32_t)(i - (size_t)s * C);
+        const uint64_t sk = kb >= 64 ? 0ull : ((uint64_t)s << kb);
+        keys[i] = (KeyT)(sk | ((cmax - cpu[i]) << mb) | (mmax - mem[i]));
+        vals[i] = j;
     }
 }
 
@@ -134,11 +141,20 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     FP_HIP(hipMemsetAsync(c->d_err, 0, 4, st));
 
     // ---- workspace ----
-    size_t sort_tmp = 0;
-    FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, sort_tmp, (uint64_t *)nullptr,
+    // device-wide sorts are sized for the widest key they may take (u64); the
+    // segmented fallback is used only when scenario + key bits exceed 64
+    size_t sort_tmp = 0, t = 0;
+    FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, SC, 0, 64, st));
+    sort_tmp = t;
+    FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, SC, 0, 32, st));
+    sort_tmp = t > sort_tmp ? t : sort_tmp;
+    FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, t, (uint64_t *)nullptr,
                                                (uint64_t *)nullptr, (uint32_t *)nullptr,
                                                (uint32_t *)nullptr, (unsigned)SC, S,
                                                (uint32_t *)nullptr, (uint32_t *)nullptr, 0, 64, st));
+    sort_tmp = t > sort_tmp ? t : sort_tmp;
     const size_t pipe_ws = fp_pipe_ws_bytes(S, C, N);
     if (pipe_ws == 0) return FP_EOVERFLOW;
     const size_t need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + pipe_ws + 16 * 256;
@@ -171,15 +187,35 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     const uint32_t kbits = cbits + mbits;
     const uint64_t cmax = cbits ? ((cbits == 64 ? ~0ull : ((1ull << cbits) - 1))) : 0ull;
     const uint64_t mmax = mbits ? ((1ull << mbits) - 1) : 0ull;
+    const uint32_t sbits = fp_bitwidth(S - 1);
     const uint32_t *order = nullptr;
-    const uint64_t *skeys = nullptr;
+    const void *skeys = nullptr;
+    uint32_t key_bytes = 8;
     if (kbits == 0) {
         k_iota_vals<<<grid_for(SC, 256), 256, 0, st>>>(SC, C, vals_out);
         FP_HIP(hipGetLastError());
         order = vals_out;
+    } else if (kbits + sbits <= 32) {
+        uint32_t *k_in = (uint32_t *)keys_in, *k_out = (uint32_t *)keys_out;
+        k_make_keys<uint32_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, kbits, mbits, cmax,
+                                                                 mmax, k_in, vals_in);
+        FP_HIP(hipGetLastError());
+        FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, k_in, k_out, vals_in, vals_out, SC, 0, kbits + sbits, st));
+        order = vals_out;
+        skeys = k_out;
+        key_bytes = 4;
+    } else if (kbits + sbits <= 64) {
+        k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, kbits, mbits, cmax,
+                                                                 mmax, keys_in, vals_in);
+        FP_HIP(hipGetLastError());
+        FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in, vals_out, SC, 0,
+                                         kbits + sbits, st));
+        order = vals_out;
+        skeys = keys_out;
     } else {
-        k_make_keys<<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, mbits, cmax,
-                                                       mmax, keys_in, vals_in);
+        // full-width cpu and mem (64 key bits): per-scenario segments
+        k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, 64, mbits, cmax,
+                                                                 mmax, keys_in, vals_in);
         FP_HIP(hipGetLastError());
         k_seg_offsets<<<(S + 1 + 255) / 256, 256, 0, st>>>(S, C, offs);
         FP_HIP(hipGetLastError());
@@ -192,7 +228,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     fp_prof_end(c, FP_K_SORT, ev);
 
     // ---- 4-5: placement + cost ----
-    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, mbits, cmax, mmax, b,
+    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, b,
                           minc == 0xFFFFFFFFu ? 1u : minc, maxc, minm == 0xFFFFFFFFu ? 1u : minm, maxm);
 }
 
