@@ -71,7 +71,7 @@ bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint
 size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N);
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
-                   const fp_batch *b,
+                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b,
                    uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm);
 
 // ---- device helpers ----

@@ -626,27 +626,35 @@ __global__ void k_cost_reduce(uint32_t S, uint32_t B, uint32_t scen_base, const 
 }
 
 // Sorted SoA for the pipeline.  cpu and mem come back out of the sorted radix keys
-// (key = [scenario] << kbits | (cmax - cpu) << mbits | (mmax - mem), coalesced; the
-// scenario field, if any, is masked off), so only req, conf and level are gathered at
-// random; without keys (all-zero demands) everything is.
+// (key = [scenario] << kbits | (cmax - c) << mbits | (mmax - m), coalesced; the scenario
+// field, if any, is masked off; c/m are the values, or their dense ranks decoded through
+// the value tables cval/mval), so only req, conf and level are gathered at random;
+// without keys (all-zero or all-equal demands) everything is.
+// XCD-aware: blocks b and b + 8 share an XCD (round-robin dispatch), so logical block
+// (b % 8) * (grid / 8) + b / 8 gives each XCD a contiguous eighth of every grid-stride
+// pass -- about ten config-4 scenarios, whose random req/conf reads then stay in that
+// XCD's 4 MB L2 instead of being fetched by all eight.
 template <class KeyT>
 __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
                                 const KeyT *__restrict__ skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax,
+                                const uint32_t *__restrict__ cval, const uint32_t *__restrict__ mval,
                                 const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
                                 const uint32_t *__restrict__ req, const uint32_t *__restrict__ conf,
                                 const uint32_t *__restrict__ level, uint32_t *__restrict__ s_cpu,
                                 uint32_t *__restrict__ s_mem, uint32_t *__restrict__ s_req,
                                 uint32_t *__restrict__ s_conf, uint32_t *__restrict__ s_idx) {
     const size_t total = (size_t)S * C;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    for (size_t i = (size_t)lb * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const size_t base = i - i % C;
         const uint32_t j = order[i];
         const size_t src = base + j;
         if (skeys) {
             const uint64_t k = skeys[i];
-            s_cpu[i] = (uint32_t)(cmax - (mbits >= 64 ? 0ull : ((k >> mbits) & cmax)));
-            s_mem[i] = (uint32_t)(mmax - (k & mmax));
+            const uint32_t c = (uint32_t)(cmax - (mbits >= 64 ? 0ull : ((k >> mbits) & cmax)));
+            const uint32_t m = (uint32_t)(mmax - (k & mmax));
+            s_cpu[i] = cval ? cval[c] : c;
+            s_mem[i] = mval ? mval[m] : m;
         } else {
             s_cpu[i] = cpu[src];
             s_mem[i] = mem[src];
@@ -703,7 +711,9 @@ static void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
 // than ~4 segments adds link latency to the FFD chain.
 constexpr uint32_t MAX_SEG_GROUPS = 40;
 constexpr size_t LDS_HALF_CU = 80 * 1024;
-constexpr uint64_t kNarrowWaves = 1024;  // S x groups at or below which stages hold one group
+// S x groups at or below which stages hold one group.  Config 3 (1 x 1M x 100k, 1563
+// groups): 160 ms with one-group stages vs 181 ms with 10-group stages (hand-scheduled loop).
+constexpr uint64_t kNarrowWaves = 4096;
 
 bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out) {
     const uint32_t NG = (N + 63) / 64;
@@ -716,9 +726,9 @@ bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint
     const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
     // FLEETPLACE_PIPE_SEG: groups per segment (tuning experiments and tests)
     const int forced_seg = getenv("FLEETPLACE_PIPE_SEG") ? atoi(getenv("FLEETPLACE_PIPE_SEG")) : 0;
-    // Few scenarios on a small table leave the GPU idle: one group (64 nodes) per
-    // stage then shortens each check (no register indexing) -- config 2 (1 x 10k x
-    // 1k): 2.39 ms vs 3.02 ms with 10-group stages.  Many scenarios keep 10-group
+    // Few scenarios leave the GPU idle: one group (64 nodes) per stage then shortens
+    // each check (no register indexing) -- config 2 (1 x 10k x 1k): 2.39 ms vs 3.02 ms
+    // with 10-group stages; config 3 (1 x 1M x 100k): 160 ms vs 181 ms.  Many scenarios keep 10-group
     // stages: stages of 1-5 groups put more waves on a CU than it can issue.
     const bool narrow = (uint64_t)S * NG <= kNarrowWaves;
     const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg
@@ -750,7 +760,7 @@ size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
 
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
-                   const fp_batch *b, uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
+                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
     uint32_t G, W, B;
     size_t lds;
     if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
@@ -779,13 +789,14 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     {
         size_t g = (SC + 255) / 256;
         if (g > 16384) g = 16384;
+        if (g >= 64) g = (g + 7) & ~(size_t)7;  // a multiple of 8: XCD-contiguous mapping
         if (key_bytes == 4)
             k_gather_sorted<uint32_t><<<(unsigned)g, 256, 0, st>>>(
-                S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, b->cpu_m, b->mem_mib, b->req_labels,
+                S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
                 b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
         else
             k_gather_sorted<uint64_t><<<(unsigned)g, 256, 0, st>>>(
-                S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, b->cpu_m, b->mem_mib, b->req_labels,
+                S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
                 b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
         FP_HIP(hipGetLastError());
     }

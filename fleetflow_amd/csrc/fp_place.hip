@@ -3,8 +3,14 @@
 //
 // Pipeline per fp_dev_place_batch call:
 //   1. k_key_bounds : max(cpu_m), max(mem_mib) over the batch (exact key width)
-//   2. k_make_keys  : key = (scenario << kb) | ((cmax-cpu) << mb) | (mmax-mem), value =
-//                     container index; u32 keys when the fields fit 32 bits, else u64
+//   1b. k_value_bitmap + k_rank_tables: when both maxima are below 2^18, the distinct
+//                     cpu and mem values of the batch, so that a key field holds the
+//                     value's dense rank (order-preserving: the sort is unchanged)
+//   2. k_make_keys  : key = (scenario << kb) | ((cmask-c) << mb) | (mmask-m), c/m the
+//                     values or their ranks, value = container index; u32 keys when the
+//                     fields fit 32 bits, else u64.  Config 4 (512 scenarios, 79 cpu and
+//                     256 mem values): 9 + 7 + 8 = 24 bits -> three 8-bit radix passes
+//                     instead of five passes over 36-bit u64 keys
 //   3. rocprim device-wide radix sort (stable; the scenario field keeps scenarios
 //      apart) => (cpu desc, mem desc, index asc) per scenario.  Keys wider than 64
 //      bits with the scenario field fall back to the segmented sort.
@@ -70,15 +76,93 @@ __global__ __launch_bounds__(256) void k_key_bounds(const uint32_t *__restrict__
     }
 }
 
+// ---- dense value ranks (order-preserving key compression) ----
+constexpr uint32_t RANK_MAX_VALUE = 1u << 18;  // per dimension: 32 KB LDS bitmap
+constexpr uint32_t RANK_WORDS = RANK_MAX_VALUE / 32;
+
+// Presence bitmaps of the cpu and mem values (value v -> bit v), built in LDS per block
+// (test before set: after the first few elements almost every bit is already there)
+// and ORed into the global bitmaps, nonzero words only.
+__global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict__ cpu,
+                                                      const uint32_t *__restrict__ mem, size_t n, uint32_t wc,
+                                                      uint32_t wm, uint32_t *__restrict__ gbc,
+                                                      uint32_t *__restrict__ gbm) {
+    extern __shared__ uint32_t lbm[];  // [wc] cpu words, then [wm] mem words
+    for (uint32_t i = threadIdx.x; i < wc + wm; i += blockDim.x) lbm[i] = 0;
+    __syncthreads();
+    uint32_t *lc = lbm, *lm = lbm + wc;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t c = cpu[i], m = mem[i];
+        const uint32_t bc = 1u << (c & 31), bmk = 1u << (m & 31);
+        if (!(lc[c >> 5] & bc)) atomicOr(&lc[c >> 5], bc);
+        if (!(lm[m >> 5] & bmk)) atomicOr(&lm[m >> 5], bmk);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x)
+        if (lc[i]) atomicOr(&gbc[i], lc[i]);
+    for (uint32_t i = threadIdx.x; i < wm; i += blockDim.x)
+        if (lm[i]) atomicOr(&gbm[i], lm[i]);
+}
+
+// One block per dimension (blockIdx.x: 0 = cpu, 1 = mem): exclusive prefix popcounts of the
+// bitmap words (rank(v) = pre[v >> 5] + popc(bm[v >> 5] & below(v))), the ascending value
+// table (val[rank] = v) and the distinct count in cnt[dim].
+__global__ __launch_bounds__(1024) void k_rank_tables(const uint32_t *__restrict__ gbc, const uint32_t *__restrict__ gbm,
+                                                      uint32_t wc, uint32_t wm, uint32_t *__restrict__ prec,
+                                                      uint32_t *__restrict__ prem, uint32_t *__restrict__ valc,
+                                                      uint32_t *__restrict__ valm, uint32_t *__restrict__ cnt) {
+    const uint32_t *bm = blockIdx.x ? gbm : gbc;
+    uint32_t *pre = blockIdx.x ? prem : prec, *val = blockIdx.x ? valm : valc;
+    const uint32_t nw = blockIdx.x ? wm : wc;
+    const uint32_t per = (nw + blockDim.x - 1) / blockDim.x, w0 = threadIdx.x * per;
+    uint32_t local = 0;
+    for (uint32_t w = w0; w < w0 + per && w < nw; ++w) local += (uint32_t)__popc(bm[w]);
+    __shared__ uint32_t part[1024];
+    part[threadIdx.x] = local;
+    __syncthreads();
+    for (uint32_t o = 1; o < blockDim.x; o <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - local;
+    for (uint32_t w = w0; w < w0 + per && w < nw; ++w) {
+        pre[w] = run;
+        uint32_t x = bm[w];
+        while (x) {
+            const uint32_t b = (uint32_t)__builtin_ctz(x);
+            x &= x - 1;
+            val[run++] = w * 32 + b;
+        }
+    }
+    if (threadIdx.x == blockDim.x - 1) cnt[blockIdx.x] = part[threadIdx.x];
+}
+
+__device__ __forceinline__ uint32_t rank_of(uint32_t v, const uint32_t *__restrict__ bm,
+                                            const uint32_t *__restrict__ pre) {
+    const uint32_t w = v >> 5;
+    return pre[w] + (uint32_t)__popc(bm[w] & ((1u << (v & 31)) - 1u));
+}
+
+// Key fields are (mask - c) and (mask - m) for descending order, c/m the values (tables
+// null) or their dense ranks.
 template <class KeyT>
 __global__ void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
                             size_t n, uint32_t C, uint32_t kb, uint32_t mb, uint64_t cmax, uint64_t mmax,
+                            const uint32_t *__restrict__ bmc, const uint32_t *__restrict__ prec,
+                            const uint32_t *__restrict__ bmm, const uint32_t *__restrict__ prem,
                             KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = (uint32_t)(i / C), j = (uint32_t)(i - (size_t)s * C);
         const uint64_t sk = kb >= 64 ? 0ull : ((uint64_t)s << kb);
-        keys[i] = (KeyT)(sk | ((cmax - cpu[i]) << mb) | (mmax - mem[i]));
+        uint32_t c = cpu[i], m = mem[i];
+        if (bmc) {
+            c = rank_of(c, bmc, prec);
+            m = rank_of(m, bmm, prem);
+        }
+        keys[i] = (KeyT)(sk | ((cmax - c) << mb) | (mmax - m));
         vals[i] = j;
     }
 }
@@ -157,7 +241,8 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     sort_tmp = t > sort_tmp ? t : sort_tmp;
     const size_t pipe_ws = fp_pipe_ws_bytes(S, C, N);
     if (pipe_ws == 0) return FP_EOVERFLOW;
-    const size_t need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + pipe_ws + 16 * 256;
+    const size_t rank_ws = 2 * (2 * RANK_WORDS * 4 + RANK_MAX_VALUE * 4) + 2 * 256;
+    const size_t need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + pipe_ws + rank_ws + 16 * 256;
     int rc = fp_ws_reserve(c, need);
     if (rc) return rc;
     fp_ws_reset(c);
@@ -168,7 +253,13 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     uint32_t *offs = (uint32_t *)fp_ws_take(c, (S + 1) * 4);
     void *tmp = fp_ws_take(c, sort_tmp + 16);
     uint32_t *bounds = (uint32_t *)fp_ws_take(c, 16);
-    if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !bounds)
+    // rank tables: bitmaps + prefix counts [2][RANK_WORDS] each, value tables, counts
+    uint32_t *rbm = (uint32_t *)fp_ws_take(c, 2 * RANK_WORDS * 4);
+    uint32_t *rpre = (uint32_t *)fp_ws_take(c, 2 * RANK_WORDS * 4);
+    uint32_t *rval = (uint32_t *)fp_ws_take(c, 2 * RANK_MAX_VALUE * 4);
+    uint32_t *rcnt = (uint32_t *)fp_ws_take(c, 16);
+    if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !bounds || !rbm || !rpre || !rval ||
+        !rcnt)
         return FP_ENOMEM;
 
     // ---- 1-3: FFD order ----
@@ -183,7 +274,31 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     FP_HIP(hipStreamSynchronize(st));
     const uint32_t maxc = ((uint32_t *)c->h_small)[0], maxm = ((uint32_t *)c->h_small)[1];
     const uint32_t minc = ((uint32_t *)c->h_small)[2], minm = ((uint32_t *)c->h_small)[3];
-    const uint32_t cbits = fp_bitwidth(maxc), mbits = fp_bitwidth(maxm);
+    uint32_t cbits = fp_bitwidth(maxc), mbits = fp_bitwidth(maxm);
+    // dense ranks when both value ranges fit the LDS bitmaps (a nonzero key only)
+    const uint32_t *bmc = nullptr, *bmm = nullptr, *prc = nullptr, *prm = nullptr;
+    const uint32_t *cval = nullptr, *mval = nullptr;
+    if (cbits + mbits > 0 && maxc < RANK_MAX_VALUE && maxm < RANK_MAX_VALUE) {
+        const uint32_t wc = maxc / 32 + 1, wm = maxm / 32 + 1;
+        FP_HIP(hipMemsetAsync(rbm, 0, 2 * RANK_WORDS * 4, st));
+        unsigned gb = grid_for(SC, 256);
+        if (gb > 1024) gb = 1024;  // each block merges its bitmaps once
+        FP_HIP(hipFuncSetAttribute((const void *)k_value_bitmap, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)((wc + wm) * 4)));
+        k_value_bitmap<<<gb, 256, (wc + wm) * 4, st>>>(b->cpu_m, b->mem_mib, SC, wc, wm, rbm, rbm + RANK_WORDS);
+        FP_HIP(hipGetLastError());
+        k_rank_tables<<<2, 1024, 0, st>>>(rbm, rbm + RANK_WORDS, wc, wm, rpre, rpre + RANK_WORDS, rval,
+                                          rval + RANK_MAX_VALUE, rcnt);
+        FP_HIP(hipGetLastError());
+        FP_HIP(hipMemcpyAsync(c->h_small, rcnt, 8, hipMemcpyDeviceToHost, st));
+        FP_HIP(hipStreamSynchronize(st));
+        const uint32_t dc = ((uint32_t *)c->h_small)[0], dm = ((uint32_t *)c->h_small)[1];
+        if (dc == 0 || dm == 0) return FP_EDEVICE;  // SC > 0: at least one value each
+        bmc = rbm; bmm = rbm + RANK_WORDS; prc = rpre; prm = rpre + RANK_WORDS;
+        cval = rval; mval = rval + RANK_MAX_VALUE;
+        cbits = fp_bitwidth(dc - 1);
+        mbits = fp_bitwidth(dm - 1);
+    }
     const uint32_t kbits = cbits + mbits;
     const uint64_t cmax = cbits ? ((cbits == 64 ? ~0ull : ((1ull << cbits) - 1))) : 0ull;
     const uint64_t mmax = mbits ? ((1ull << mbits) - 1) : 0ull;
@@ -198,7 +313,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     } else if (kbits + sbits <= 32) {
         uint32_t *k_in = (uint32_t *)keys_in, *k_out = (uint32_t *)keys_out;
         k_make_keys<uint32_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, kbits, mbits, cmax,
-                                                                 mmax, k_in, vals_in);
+                                                                 mmax, bmc, prc, bmm, prm, k_in, vals_in);
         FP_HIP(hipGetLastError());
         FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, k_in, k_out, vals_in, vals_out, SC, 0, kbits + sbits, st));
         order = vals_out;
@@ -206,7 +321,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         key_bytes = 4;
     } else if (kbits + sbits <= 64) {
         k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, kbits, mbits, cmax,
-                                                                 mmax, keys_in, vals_in);
+                                                                 mmax, bmc, prc, bmm, prm, keys_in, vals_in);
         FP_HIP(hipGetLastError());
         FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in, vals_out, SC, 0,
                                          kbits + sbits, st));
@@ -215,7 +330,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     } else {
         // full-width cpu and mem (64 key bits): per-scenario segments
         k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, 64, mbits, cmax,
-                                                                 mmax, keys_in, vals_in);
+                                                                 mmax, bmc, prc, bmm, prm, keys_in, vals_in);
         FP_HIP(hipGetLastError());
         k_seg_offsets<<<(S + 1 + 255) / 256, 256, 0, st>>>(S, C, offs);
         FP_HIP(hipGetLastError());
@@ -228,7 +343,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     fp_prof_end(c, FP_K_SORT, ev);
 
     // ---- 4-5: placement + cost ----
-    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, b,
+    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, cval, mval, b,
                           minc == 0xFFFFFFFFu ? 1u : minc, maxc, minm == 0xFFFFFFFFu ? 1u : minm, maxm);
 }
 

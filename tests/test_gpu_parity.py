@@ -249,6 +249,49 @@ def test_config4_scenarios_full_size(planner, O):
     assert int(best.item()) == int(np.argmin(costs))
 
 
+@pytest.mark.parametrize("case", ["all_equal", "cpu_const", "mem_const", "rank_limit", "past_rank_limit",
+                                  "dense_wide", "zero_mix"])
+def test_ffd_sort_key_compression(case, planner, O):
+    """The FFD order uses dense value ranks as key fields when both maxima are below
+    2^18 (fp_place.hip k_value_bitmap/k_rank_tables) and the raw values otherwise;
+    either way the order, and so the plan, must be the oracle's."""
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    C, N = 3000, 400
+    lim = 1 << 18
+    cpu = rng.integers(1, 5000, C)
+    mem = rng.integers(1, 20000, C)
+    if case == "all_equal":
+        cpu[:] = 700; mem[:] = 900
+    elif case == "cpu_const":
+        cpu[:] = 1234
+    elif case == "mem_const":
+        mem[:] = 77
+    elif case == "rank_limit":
+        cpu[:5] = lim - 1; mem[-5:] = lim - 1
+    elif case == "past_rank_limit":
+        cpu[:5] = lim; mem[-5:] = lim - 1
+    elif case == "dense_wide":
+        cpu = rng.integers(0, lim, C); mem = rng.integers(0, lim, C)
+    elif case == "zero_mix":
+        cpu[::3] = 0; mem[::5] = 0
+    cont = (cpu.astype(np.uint32), mem.astype(np.uint32), np.zeros(C, np.uint32),
+            (rng.random(C) < 0.2).astype(np.uint32) << rng.integers(0, 32, C).astype(np.uint32))
+    big = int(max(cpu.max(), mem.max())) * 4 + 10
+    nodes = (rng.integers(0, big, N).astype(np.uint32), rng.integers(0, big, N).astype(np.uint32),
+             np.zeros(N, np.uint32), np.zeros(N, np.uint32), (rng.random(N) < 0.95).astype(np.uint8))
+    _check_ffd(planner, O, cont, nodes)
+    # and batched (scenario field in the key), scenarios with different value sets
+    S = 5
+    conts = [tuple(np.roll(a, 17 * s) if i < 2 else a for i, a in enumerate(cont)) for s in range(S)]
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    assign, reason, cost, after = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
+                                                      [np.tile(a, S) for a in nodes], scen_base=0)
+    for s in range(S):
+        ea, er, _, _ = O.place(conts[s], nodes)
+        assert np.array_equal(assign[s * C:(s + 1) * C], ea)
+        assert np.array_equal(reason[s * C:(s + 1) * C], er)
+
+
 # ---- segmented pipeline: N beyond one workgroup's LDS (> 80 groups of 64 nodes) ----
 @pytest.mark.parametrize("C,N,flags", [(20_000, 6_000, 7), (30_000, 20_000, 7), (2_000, 100_000, 7),
                                        (60_000, 33_000, 3), (5_000, 5_121, 7)])
