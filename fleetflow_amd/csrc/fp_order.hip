@@ -8,6 +8,8 @@
 //    schedule (atomic order inside a level) cannot change the result.
 #include "fp_internal.h"
 #include <rocprim/device/device_radix_sort.hpp>
+#include <stdlib.h>
+#include <string.h>
 
 namespace {
 
@@ -166,6 +168,310 @@ __global__ void k_lvl_final(const uint32_t *__restrict__ indeg, uint32_t V, uint
     if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(ncyc, (uint32_t)__popcll(m));
 }
 
+// ---- asynchronous levelizer (no level barriers) -------------------------------------
+// A persistent grid works a sharded queue of ready vertices.  Per vertex v a packed
+// state word holds (max level seen << 32 | parents still to come); a parent u relaxes
+// the edge u -> v with one CAS (level max(., level(u)+1), count - 1).  The CAS that
+// takes the count to zero owns v: its level is final (every parent's update landed
+// in the same word before).  The owner continues with its first ready child in the
+// same lane (a chain never touches the queue) and pushes the others.  So a chain of
+// depth D costs D dependent (row_ptr, col, CAS) round trips, not D kernel launches.
+// Termination: done[] counts queue items whose lane (and continuation chain) has
+// finished, tail[] counts pushed items; done == tail means nothing is in flight and
+// nothing can be pushed again.  One monitor lane checks it and raises `fin`.
+constexpr uint32_t kShards = 8;           // queues (blocks b and b+8 share an XCD)
+constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B lines)
+constexpr uint64_t kQEmpty = ~0ull;
+constexpr uint32_t kCoopEdges = 16;       // edges left at which the wave expands a vertex together
+constexpr uint32_t kLaneEdges = 2;        // edges a lane relaxes per round
+// ctl layout (u32 index): head[s] = s*32, tail[s] = (8+s)*32, done[s] = (16+s)*32,
+// fin = 24*32, abort = 25*32, maxlvl = 26*32
+constexpr uint32_t kCtlWords = 27 * kCtlStride;
+
+__device__ __forceinline__ uint64_t ag_ld64(const uint64_t *p) {
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ag_ld32(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (an RMW)
+    return __hip_atomic_fetch_add(p, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sources (in-degree 0) with out-edges go to the queues; every other vertex starts
+// at level NONE (a source without out-edges is final here).
+__global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
+                                 const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t *__restrict__ level,
+                                 uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl) {
+    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = v < V;
+    uint32_t l0 = 0, deg = 0;
+    bool src = false;
+    if (in) {
+        l0 = hd[v] ? 1u : 0u;
+        deg = row_ptr[v + 1] - row_ptr[v];
+        src = indeg[v] == 0;
+        state[v] = ((uint64_t)l0 << 32) | indeg[v];
+        level[v] = src && deg == 0 ? l0 : FP_NONE;
+    }
+    const bool push = src && deg != 0;
+    const uint64_t m = __ballot(push);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(m);
+    const uint32_t sh = (uint32_t)((v >> 6) % kShards);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&ctl[(kShards + sh) * kCtlStride], (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (push) Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)l0 << 32) | v;
+}
+
+__global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
+                                                  uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
+                                                  uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
+                                                  uint32_t *__restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t sh = blockIdx.x % kShards;
+    uint32_t *head = &ctl[sh * kCtlStride];
+    uint32_t *done = &ctl[(2 * kShards + sh) * kCtlStride];
+    uint32_t *fin = &ctl[24 * kCtlStride], *abortw = &ctl[25 * kCtlStride];
+    const uint64_t *q = Q + (size_t)sh * V;  // claims come from the block's own shard
+    uint32_t rr = blockIdx.x / kShards;       // pushes rotate over all shards (load spreading)
+    const bool monitor = blockIdx.x == 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // lane state: a claim on a queue slot, or an item u (level lu) with edges [e, e1),
+    // and at most one continuation cw (level cl, edges [ce, ce1) prefetched)
+    bool has_claim = false, has_item = false;
+    uint32_t slot = 0, u = 0, lu = 0, e = 0, e1 = 0, my_max = 0, idle = 0;
+    uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    // deferred pushes (see below): entries, offsets, the reserved base (lane 0)
+    bool pend[kLaneEdges];
+    uint32_t pofs[kLaneEdges], pbase = 0, npend = 0;
+    uint64_t pent[kLaneEdges];
+    uint64_t *pq = Q;
+    while (true) {
+        if (npend) {
+            const uint32_t base = __shfl(pbase, 0);
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneEdges; ++k)
+                if (pend[k]) __hip_atomic_store(&pq[base + pofs[k]], pent[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            npend = 0;
+        }
+        // one round: the poll of a claimed slot and one edge step of an item are issued
+        // together, so a busy wave's polls cost no extra round trip
+        uint64_t x = kQEmpty;
+        if (has_claim && slot < V) x = ag_ld64(&q[slot]);
+        // a vertex with many edges left (a chain head feeding a whole fan-out layer) is
+        // expanded by the whole wave, 64 edges per step, its ready children all pushed
+        uint64_t bm = __ballot(has_item && e1 - e >= kCoopEdges);
+        while (bm) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(bm);
+            bm &= bm - 1;
+            const uint32_t blu = __builtin_amdgcn_readlane(lu, L), be0 = __builtin_amdgcn_readlane(e, L),
+                           be1 = __builtin_amdgcn_readlane(e1, L);
+            for (uint32_t base = be0; base < be1; base += 64) {
+                const uint32_t ee = base + lane;
+                bool rdy = false;
+                uint32_t ww = 0;
+                uint64_t cur = 0;
+                if (ee < be1) {
+                    ww = col[ee];
+                    uint64_t exp = (1ull << 32) | 1ull;
+                    while (true) {
+                        const uint32_t nl = max((uint32_t)(exp >> 32), blu + 1u);
+                        const uint64_t nv = ((uint64_t)nl << 32) | (uint32_t)((uint32_t)exp - 1u);
+                        uint64_t obs = exp;
+                        if (__hip_atomic_compare_exchange_strong(&state[ww], &obs, nv, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            cur = nv;
+                            break;
+                        }
+                        exp = obs;
+                    }
+                    rdy = (uint32_t)cur == 0u;
+                }
+                const uint64_t rm = __ballot(rdy);
+                if (rm) {
+                    const uint32_t leader = (uint32_t)__builtin_ctzll(rm);
+                    uint32_t b0 = 0;
+                    const uint32_t ps = (sh + ++rr) % kShards;
+                    if (lane == leader) b0 = atomicAdd(&ctl[(kShards + ps) * kCtlStride], (uint32_t)__popcll(rm));
+                    b0 = __shfl(b0, (int)leader);
+                    if (rdy)
+                        __hip_atomic_store(&Q[(size_t)ps * V + b0 + (uint32_t)__popcll(rm & lt)],
+                                           (cur & 0xFFFFFFFF00000000ull) | ww, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (lane == L) e = e1;  // the step below finishes (or continues) the item
+        }
+        // per-lane step: up to kLaneEdges edges at once (loads and first CAS attempts all in
+        // flight together), so a chain link with a few fan-out children still takes one round
+        bool ready[kLaneEdges], fin_item = false;
+        uint32_t w[kLaneEdges], wl[kLaneEdges];
+#pragma unroll
+        for (uint32_t k = 0; k < kLaneEdges; ++k) ready[k] = false;
+        if (has_item) {
+            const uint32_t ne = min(e1 - e, kLaneEdges);
+            uint32_t p0[kLaneEdges], p1[kLaneEdges];
+            uint64_t cur[kLaneEdges], obs[kLaneEdges];
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneEdges; ++k)
+                if (k < ne) w[k] = col[e + k];
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneEdges; ++k)
+                if (k < ne) { p0[k] = row_ptr[w[k]]; p1[k] = row_ptr[w[k] + 1]; }  // speculative continuation edges
+            // first attempt guesses an untouched vertex with deps and one parent (a chain link)
+            const uint64_t g = (1ull << 32) | 1ull;
+            const uint64_t gn = ((uint64_t)max(1u, lu + 1u) << 32);
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneEdges; ++k) {
+                if (k < ne) {
+                    obs[k] = g;
+                    cur[k] = __hip_atomic_compare_exchange_strong(&state[w[k]], &obs[k], gn, __ATOMIC_RELAXED,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 ? gn : kQEmpty;
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneEdges; ++k) {
+                if (k < ne) {
+                    uint64_t exp = obs[k];
+                    while (cur[k] == kQEmpty) {  // retry with the observed word
+                        const uint32_t nl = max((uint32_t)(exp >> 32), lu + 1u);
+                        const uint64_t nv = ((uint64_t)nl << 32) | (uint32_t)((uint32_t)exp - 1u);
+                        uint64_t o = exp;
+                        if (__hip_atomic_compare_exchange_strong(&state[w[k]], &o, nv, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                            cur[k] = nv;
+                        else
+                            exp = o;
+                    }
+                    if ((uint32_t)cur[k] == 0u) {
+                        wl[k] = (uint32_t)(cur[k] >> 32);
+                        if (cw == FP_NONE) {
+                            cw = w[k]; cl = wl[k]; ce = p0[k]; ce1 = p1[k];
+                        } else {
+                            ready[k] = true;
+                        }
+                    }
+                }
+            }
+            e += ne;
+            if (e >= e1) {
+                if (cw != FP_NONE) {  // continue down the chain in this lane
+                    u = cw; lu = cl; e = ce; e1 = ce1;
+                    cw = FP_NONE;
+                    level[u] = lu;
+                    my_max = max(my_max, lu);
+                } else {
+                    has_item = false;
+                    fin_item = true;
+                }
+            }
+        }
+        if (x != kQEmpty) {
+            has_claim = false;
+            has_item = true;
+            u = (uint32_t)x;
+            lu = (uint32_t)(x >> 32);
+            e = row_ptr[u];
+            e1 = row_ptr[u + 1];
+            level[u] = lu;
+            my_max = max(my_max, lu);
+        }
+        // claim one queue slot per lane without work (wave-aggregated); issued before the
+        // pushes so that its round trip overlaps theirs (the slot is first read next round)
+        {
+            const bool need = !has_claim && !has_item;
+            const uint64_t nm = __ballot(need);
+            if (nm) {
+                const uint32_t leader = (uint32_t)__builtin_ctzll(nm);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(head, (uint32_t)__popcll(nm));
+                base = __shfl(base, (int)leader);
+                if (need) {
+                    slot = base + (uint32_t)__popcll(nm & lt);
+                    has_claim = true;
+                }
+            }
+        }
+        // pushes, deferred by one round: this round reserves the queue slots (the add's
+        // result is not waited for), the next round stores the entries -- the reservation's
+        // round trip overlaps the next round's loads instead of adding to this one
+        uint64_t rm[kLaneEdges];
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kLaneEdges; ++k) {
+            rm[k] = __ballot(ready[k]);
+            tot += (uint32_t)__popcll(rm[k]);
+        }
+        if (tot) {
+            const uint32_t ps = (sh + ++rr) % kShards;
+            if (lane == 0) pbase = atomicAdd(&ctl[(kShards + ps) * kCtlStride], tot);
+            pq = Q + (size_t)ps * V;
+            uint32_t run = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneEdges; ++k) {
+                pend[k] = ready[k];
+                pofs[k] = run + (uint32_t)__popcll(rm[k] & lt);
+                pent[k] = ((uint64_t)wl[k] << 32) | w[k];
+                run += (uint32_t)__popcll(rm[k]);
+            }
+            npend = 1;
+        }
+        const uint64_t fm = __ballot(fin_item);
+        // relaxed, not waited for: this wave's push reservations (tail adds) have already
+        // returned, and quiescence is decided on the counters alone
+        if (fm && lane == (uint32_t)__builtin_ctzll(fm))
+            __hip_atomic_fetch_add(done, (uint32_t)__popcll(fm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__ballot(has_item) || fm || npend) {
+            idle = 0;
+            continue;
+        }
+        // idle round: every lane holds a claim on an empty (or past-the-end) slot
+        uint32_t stop = 0;
+        if (lane == 0) {
+            if (monitor) {
+                uint32_t d = 0, t = 0;
+                for (uint32_t k = 0; k < kShards; ++k) d += ag_rmw_rd(&ctl[(2 * kShards + k) * kCtlStride]);
+                for (uint32_t k = 0; k < kShards; ++k) t += ag_rmw_rd(&ctl[(kShards + k) * kCtlStride]);
+                if (d == t) {
+                    __hip_atomic_store(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 1;
+                }
+            }
+            if (ag_ld32(fin) || ag_ld32(abortw)) stop = 1;
+            if (!stop && __builtin_amdgcn_s_memrealtime() - t_start > 100ull * 1000 * 1000 * 60) {  // 60 s guard
+                __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicMax(err, (uint32_t)(-FP_EDEVICE));
+                stop = 1;
+            }
+        }
+        if (__shfl(stop, 0)) break;
+        ++idle;
+        if (idle < 16) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(8);
+    }
+    for (int o = 32; o > 0; o >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor((int)my_max, o));
+    if (lane == 0 && my_max) atomicMax(&ctl[26 * kCtlStride], my_max);
+}
+
+// level -> sort keys; vertices never finished (cycle members and everything behind
+// them) are NONE and take cyc_key; counts them.
+__global__ void k_lvl_async_final(uint32_t V, uint32_t cyc_key, const uint32_t *__restrict__ level,
+                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                  uint32_t *__restrict__ ncyc) {
+    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool cyc = v < V && level[v] == FP_NONE;
+    if (v < V) {
+        keys[v] = cyc ? cyc_key : level[v];
+        vals[v] = (uint32_t)v;
+    }
+    const uint64_t m = __ballot(cyc);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(ncyc, (uint32_t)__popcll(m));
+}
+
 inline unsigned blocks_for(size_t n, unsigned b) {
     size_t g = (n + b - 1) / b;
     return (unsigned)(g ? g : 1);
@@ -215,7 +521,8 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
                                      (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)V, 0, 32, st));
     // cnt[L] = frontier size of level L (one counter per possible level: <= V + 1)
     const size_t ncnt = (size_t)V + 2;
-    int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + 16 * 256);
+    int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + (size_t)V * 8 * (1 + kShards) +
+                                   kCtlWords * 4 + 20 * 256);
     if (rc) return rc;
     fp_ws_reset(c);
     uint32_t *indeg = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
@@ -240,6 +547,41 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         k_indeg<<<blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192, 256, 0, st>>>(
             g->col, E, V, indeg, c->d_err);
         FP_HIP(hipGetLastError());
+    }
+    // FLEETPLACE_LEVELIZE=levels: the level-synchronous schedule (one launch per level)
+    static const bool level_sync = getenv("FLEETPLACE_LEVELIZE") && !strcmp(getenv("FLEETPLACE_LEVELIZE"), "levels");
+    if (!level_sync) {
+        if ((uint64_t)V + 65536ull * 64 >= 0xFFFFFFFFull) return FP_EOVERFLOW;  // queue heads stay below 2^32
+        uint64_t *state = (uint64_t *)fp_ws_take(c, (size_t)V * 8);
+        uint64_t *Q = (uint64_t *)fp_ws_take(c, (size_t)V * 8 * kShards);
+        uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
+        if (!state || !Q || !actl) return FP_ENOMEM;
+        FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
+        FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
+        k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl);
+        FP_HIP(hipGetLastError());
+        FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
+        FP_HIP(hipStreamSynchronize(st));
+        if (((uint32_t *)c->h_small)[0]) return -(int)((uint32_t *)c->h_small)[0];
+        if (E) {
+            // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
+            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, g->col, V, state, Q, actl, level, c->d_err);
+            FP_HIP(hipGetLastError());
+        }
+        FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
+        FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &actl[26 * kCtlStride], 4, hipMemcpyDeviceToHost, st));
+        FP_HIP(hipStreamSynchronize(st));
+        if (((uint32_t *)c->h_small)[0]) return -(int)((uint32_t *)c->h_small)[0];
+        const uint32_t maxl = ((uint32_t *)c->h_small)[2];
+        // levels <= max(maxl, 1); the cycle key sorts after every level
+        const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
+        k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, cyc_key, level, keys, vals, ncyc);
+        FP_HIP(hipGetLastError());
+        FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys, keys_out, vals, order, (size_t)V, 0,
+                                         fp_bitwidth(cyc_key), st));
+        if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
+        fp_prof_end(c, FP_K_LEVEL, ev);
+        return FP_OK;
     }
     k_lvl_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, V, level, fa, &cnt[0]);
     FP_HIP(hipGetLastError());

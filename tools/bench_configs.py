@@ -173,6 +173,8 @@ def main():
         if "3" in only:
             print(json.dumps(ffd_config(p, dev, "3: 1M containers x 100k nodes, labels + anti-affinity",
                                         SEED + 3, 1_000_000, 100_000, 7, args.reps, cpu)), flush=True)
+        if "l" in only:  # levelization alone
+            print(json.dumps(levelize_config(p, dev, args.reps, cpu)[0]), flush=True)
         if "5" in only:
             lv, level = levelize_config(p, dev, args.reps, cpu)
             print(json.dumps(lv), flush=True)
