@@ -56,6 +56,47 @@ def test_levelize_random_dags(params, planner, O):
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
+def _csr(V, edges):
+    edges = sorted(edges, key=lambda t: t[0])  # stable: per-dep order kept
+    rp = np.zeros(V + 1, np.uint32)
+    for d, _ in edges:
+        rp[d + 1] += 1
+    rp = np.cumsum(rp).astype(np.uint32)
+    col = np.array([t for _, t in edges], np.uint32)
+    return rp, col
+
+
+@pytest.mark.parametrize("shape", ["star", "dup_and_self", "long_chain_fanout", "wide_hubs"])
+def test_levelize_async_shapes(shape, planner, O):
+    """Shapes aimed at the asynchronous levelizer's paths: wave-cooperative expansion
+    (a vertex with thousands of dependents), duplicate edges and self loops (CAS
+    retries, CYCLE), chain continuation with fan-out side edges, many hubs."""
+    rng = np.random.default_rng(7)
+    if shape == "star":
+        V = 20_000
+        edges = [(0, v) for v in range(1, V)] + [(v, v + 1) for v in range(1, 200)]
+    elif shape == "dup_and_self":
+        V = 3000
+        edges = [(v, v + 1) for v in range(0, V - 1, 2)] * 2 + [(5, 5), (17, 17)]
+        edges += [(int(a), int(b)) for a, b in zip(rng.integers(0, V // 2, 2000), rng.integers(V // 2, V, 2000))]
+    elif shape == "long_chain_fanout":
+        V = 30_000
+        edges = [(v, v + 1) for v in range(0, 5000)]
+        edges += [(int(a), int(b)) for a, b in zip(rng.integers(0, 5000, 40_000), rng.integers(5001, V, 40_000))]
+    else:
+        V = 50_000
+        hubs = rng.integers(0, 100, 200_000)
+        edges = [(int(h), int(t)) for h, t in zip(hubs, rng.integers(100, V, 200_000))]
+        edges += [(int(t), int(t) + 1) for t in range(100, V - 1, 3)]
+    rp, col = _csr(V, edges)
+    hd = np.zeros(V, np.uint8)
+    hd[np.unique(col)] = 1
+    hd[rng.integers(0, V, V // 10)] = 1  # deps outside the target set
+    level, order, ncyc = planner.levelize(rp, col, hd)
+    el, eo, en = O.levelize(rp, col, hd)
+    assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
 def test_levelize_config5_full_size(planner, O):
     """BASELINE config 5: 1M vertices (1000 chains x 500 + 50 layers x 10k), 333 3-cycles."""
     rp, col, hd = O.gen_dag(SEED + 5, 1000, 500, 50, 10_000, 333)
