@@ -643,25 +643,56 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
                                 const uint32_t *__restrict__ level, uint32_t *__restrict__ s_cpu,
                                 uint32_t *__restrict__ s_mem, uint32_t *__restrict__ s_req,
                                 uint32_t *__restrict__ s_conf, uint32_t *__restrict__ s_idx) {
-    const size_t total = (size_t)S * C;
+    // S * C < 2^32 (fp_dev_place_batch_impl checks): 32-bit index arithmetic, and four
+    // independent elements per thread in flight (the req/conf gathers are dependent loads)
+    const uint32_t total = S * C, stride = gridDim.x * blockDim.x;
     const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    for (size_t i = (size_t)lb * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t base = i - i % C;
-        const uint32_t j = order[i];
-        const size_t src = base + j;
-        if (skeys) {
-            const uint64_t k = skeys[i];
-            const uint32_t c = (uint32_t)(cmax - (mbits >= 64 ? 0ull : ((k >> mbits) & cmax)));
-            const uint32_t m = (uint32_t)(mmax - (k & mmax));
-            s_cpu[i] = cval ? cval[c] : c;
-            s_mem[i] = mval ? mval[m] : m;
-        } else {
-            s_cpu[i] = cpu[src];
-            s_mem[i] = mem[src];
+    for (size_t i0 = (size_t)lb * blockDim.x + threadIdx.x; i0 < total; i0 += 4 * (size_t)stride) {
+        uint32_t j[4], src[4], r[4], f[4], cy[4], cv[4], mv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + (size_t)u * stride;
+            if (i < total) j[u] = order[i];
         }
-        s_req[i] = req[src];
-        s_conf[i] = conf[src];
-        s_idx[i] = j | ((level && level[src] == FP_NONE) ? CYC : 0u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + (size_t)u * stride;
+            if (i < total) {
+                src[u] = (uint32_t)i - (uint32_t)i % C + j[u];  // i < total < 2^32
+                if (skeys) {
+                    const uint64_t k = skeys[i];
+                    cv[u] = (uint32_t)(cmax - (mbits >= 64 ? 0ull : ((k >> mbits) & cmax)));
+                    mv[u] = (uint32_t)(mmax - (k & mmax));
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + (size_t)u * stride;
+            if (i < total) {
+                r[u] = req[src[u]];
+                f[u] = conf[src[u]];
+                cy[u] = (level && level[src[u]] == FP_NONE) ? CYC : 0u;
+                if (skeys) {
+                    if (cval) cv[u] = cval[cv[u]];
+                    if (mval) mv[u] = mval[mv[u]];
+                } else {
+                    cv[u] = cpu[src[u]];
+                    mv[u] = mem[src[u]];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + (size_t)u * stride;
+            if (i < total) {
+                s_cpu[i] = cv[u];
+                s_mem[i] = mv[u];
+                s_req[i] = r[u];
+                s_conf[i] = f[u];
+                s_idx[i] = j[u] | cy[u];
+            }
+        }
     }
 }
 
@@ -787,7 +818,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         return FP_ENOMEM;
     FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * 128, st));
     {
-        size_t g = (SC + 255) / 256;
+        size_t g = (SC + 1023) / 1024;  // four elements per thread per pass
         if (g > 16384) g = 16384;
         if (g >= 64) g = (g + 7) & ~(size_t)7;  // a multiple of 8: XCD-contiguous mapping
         if (key_bytes == 4)

@@ -80,28 +80,44 @@ __global__ __launch_bounds__(256) void k_key_bounds(const uint32_t *__restrict__
 constexpr uint32_t RANK_MAX_VALUE = 1u << 18;  // per dimension: 32 KB LDS bitmap
 constexpr uint32_t RANK_WORDS = RANK_MAX_VALUE / 32;
 
-// Presence bitmaps of the cpu and mem values (value v -> bit v), built in LDS per block
-// (test before set: after the first few elements almost every bit is already there)
-// and ORed into the global bitmaps, nonzero words only.
+// Presence bitmaps of the cpu and mem values (value v -> bit v, v < 2^18), built in LDS
+// per block (test before set: after the first few elements almost every bit is already
+// there) and ORed into the global bitmaps, nonzero words only.  A value >= 2^18 sets
+// *over (the caller then falls back to raw-value keys and k_key_bounds).  The bounds
+// the placement needs (max, min positive) come out of the bitmaps (k_rank_tables), so
+// this one pass over cpu/mem replaces the bounds pass.
 __global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict__ cpu,
-                                                      const uint32_t *__restrict__ mem, size_t n, uint32_t wc,
-                                                      uint32_t wm, uint32_t *__restrict__ gbc,
-                                                      uint32_t *__restrict__ gbm) {
-    extern __shared__ uint32_t lbm[];  // [wc] cpu words, then [wm] mem words
-    for (uint32_t i = threadIdx.x; i < wc + wm; i += blockDim.x) lbm[i] = 0;
+                                                      const uint32_t *__restrict__ mem, size_t n,
+                                                      uint32_t *__restrict__ gbc, uint32_t *__restrict__ gbm,
+                                                      uint32_t *__restrict__ over) {
+    extern __shared__ uint32_t lbm[];  // [RANK_WORDS] cpu words, then [RANK_WORDS] mem words
+    for (uint32_t i = threadIdx.x; i < 2 * RANK_WORDS; i += blockDim.x) lbm[i] = 0;
     __syncthreads();
-    uint32_t *lc = lbm, *lm = lbm + wc;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t c = cpu[i], m = mem[i];
+    uint32_t *lc = lbm, *lm = lbm + RANK_WORDS;
+    bool big = false;
+    auto add = [&](uint32_t c, uint32_t m) {
+        if ((c | m) >= RANK_MAX_VALUE) { big = true; return; }
         const uint32_t bc = 1u << (c & 31), bmk = 1u << (m & 31);
         if (!(lc[c >> 5] & bc)) atomicOr(&lc[c >> 5], bc);
         if (!(lm[m >> 5] & bmk)) atomicOr(&lm[m >> 5], bmk);
+    };
+    const size_t stride = (size_t)gridDim.x * blockDim.x, t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t head = 0;
+    if (((reinterpret_cast<uintptr_t>(cpu) | reinterpret_cast<uintptr_t>(mem)) & 15u) == 0) {
+        const uint4 *c4 = reinterpret_cast<const uint4 *>(cpu), *m4 = reinterpret_cast<const uint4 *>(mem);
+        for (size_t i = t; i < n / 4; i += stride) {
+            const uint4 c = c4[i], m = m4[i];
+            add(c.x, m.x); add(c.y, m.y); add(c.z, m.z); add(c.w, m.w);
+        }
+        head = n / 4 * 4;
     }
+    for (size_t i = head + t; i < n; i += stride) add(cpu[i], mem[i]);
+    if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(over, 1u);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x)
+    for (uint32_t i = threadIdx.x; i < RANK_WORDS; i += blockDim.x) {
         if (lc[i]) atomicOr(&gbc[i], lc[i]);
-    for (uint32_t i = threadIdx.x; i < wm; i += blockDim.x)
         if (lm[i]) atomicOr(&gbm[i], lm[i]);
+    }
 }
 
 // One block per dimension (blockIdx.x: 0 = cpu, 1 = mem): exclusive prefix popcounts of the
@@ -136,7 +152,13 @@ __global__ __launch_bounds__(1024) void k_rank_tables(const uint32_t *__restrict
             val[run++] = w * 32 + b;
         }
     }
-    if (threadIdx.x == blockDim.x - 1) cnt[blockIdx.x] = part[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) {
+        const uint32_t d = part[threadIdx.x];
+        cnt[blockIdx.x] = d;                                       // distinct values
+        cnt[2 + blockIdx.x] = d ? val[d - 1] : 0u;                 // max value
+        cnt[4 + blockIdx.x] = d == 0 ? 0xFFFFFFFFu : val[0] ? val[0] : d > 1 ? val[1] : 0xFFFFFFFFu;  // min positive
+    }
 }
 
 __device__ __forceinline__ uint32_t rank_of(uint32_t v, const uint32_t *__restrict__ bm,
@@ -155,7 +177,7 @@ __global__ void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__
                             KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t s = (uint32_t)(i / C), j = (uint32_t)(i - (size_t)s * C);
+        const uint32_t s = (uint32_t)i / C, j = (uint32_t)i - s * C;  // n = S * C < 2^32
         const uint64_t sk = kb >= 64 ? 0ull : ((uint64_t)s << kb);
         uint32_t c = cpu[i], m = mem[i];
         if (bmc) {
@@ -257,7 +279,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     uint32_t *rbm = (uint32_t *)fp_ws_take(c, 2 * RANK_WORDS * 4);
     uint32_t *rpre = (uint32_t *)fp_ws_take(c, 2 * RANK_WORDS * 4);
     uint32_t *rval = (uint32_t *)fp_ws_take(c, 2 * RANK_MAX_VALUE * 4);
-    uint32_t *rcnt = (uint32_t *)fp_ws_take(c, 16);
+    uint32_t *rcnt = (uint32_t *)fp_ws_take(c, 32);
     if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !bounds || !rbm || !rpre || !rval ||
         !rcnt)
         return FP_ENOMEM;
@@ -265,34 +287,41 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     // ---- 1-3: FFD order ----
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_SORT, &ev);
-    FP_HIP(hipMemsetAsync(bounds, 0, 8, st));
-    FP_HIP(hipMemsetAsync(bounds + 2, 0xFF, 8, st));
-    k_key_bounds<<<grid_for((SC + 3) / 4, 256) < 2048 ? grid_for((SC + 3) / 4, 256) : 2048, 256, 0, st>>>(
-        b->cpu_m, b->mem_mib, SC, bounds);
-    FP_HIP(hipGetLastError());
-    FP_HIP(hipMemcpyAsync(c->h_small, bounds, 16, hipMemcpyDeviceToHost, st));
-    FP_HIP(hipStreamSynchronize(st));
-    const uint32_t maxc = ((uint32_t *)c->h_small)[0], maxm = ((uint32_t *)c->h_small)[1];
-    const uint32_t minc = ((uint32_t *)c->h_small)[2], minm = ((uint32_t *)c->h_small)[3];
-    uint32_t cbits = fp_bitwidth(maxc), mbits = fp_bitwidth(maxm);
-    // dense ranks when both value ranges fit the LDS bitmaps (a nonzero key only)
-    const uint32_t *bmc = nullptr, *bmm = nullptr, *prc = nullptr, *prm = nullptr;
-    const uint32_t *cval = nullptr, *mval = nullptr;
-    if (cbits + mbits > 0 && maxc < RANK_MAX_VALUE && maxm < RANK_MAX_VALUE) {
-        const uint32_t wc = maxc / 32 + 1, wm = maxm / 32 + 1;
-        FP_HIP(hipMemsetAsync(rbm, 0, 2 * RANK_WORDS * 4, st));
-        unsigned gb = grid_for(SC, 256);
+    // value bitmaps -> dense ranks, distinct counts and bounds in one pass (values < 2^18)
+    FP_HIP(hipMemsetAsync(rbm, 0, 2 * RANK_WORDS * 4, st));
+    FP_HIP(hipMemsetAsync(rcnt, 0, 32, st));
+    {
+        unsigned gb = grid_for((SC + 3) / 4, 256);
         if (gb > 1024) gb = 1024;  // each block merges its bitmaps once
         FP_HIP(hipFuncSetAttribute((const void *)k_value_bitmap, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)((wc + wm) * 4)));
-        k_value_bitmap<<<gb, 256, (wc + wm) * 4, st>>>(b->cpu_m, b->mem_mib, SC, wc, wm, rbm, rbm + RANK_WORDS);
+                                   (int)(2 * RANK_WORDS * 4)));
+        k_value_bitmap<<<gb, 256, 2 * RANK_WORDS * 4, st>>>(b->cpu_m, b->mem_mib, SC, rbm, rbm + RANK_WORDS, rcnt + 6);
         FP_HIP(hipGetLastError());
-        k_rank_tables<<<2, 1024, 0, st>>>(rbm, rbm + RANK_WORDS, wc, wm, rpre, rpre + RANK_WORDS, rval,
+        k_rank_tables<<<2, 1024, 0, st>>>(rbm, rbm + RANK_WORDS, RANK_WORDS, RANK_WORDS, rpre, rpre + RANK_WORDS, rval,
                                           rval + RANK_MAX_VALUE, rcnt);
         FP_HIP(hipGetLastError());
-        FP_HIP(hipMemcpyAsync(c->h_small, rcnt, 8, hipMemcpyDeviceToHost, st));
+    }
+    FP_HIP(hipMemcpyAsync(c->h_small, rcnt, 28, hipMemcpyDeviceToHost, st));
+    FP_HIP(hipStreamSynchronize(st));
+    const uint32_t *hs = (const uint32_t *)c->h_small;
+    const bool ranks = hs[6] == 0;
+    uint32_t maxc = hs[2], maxm = hs[3], minc = hs[4], minm = hs[5];
+    const uint32_t dc = hs[0], dm = hs[1];
+    if (!ranks) {  // a value >= 2^18: raw-value keys, exact bounds
+        FP_HIP(hipMemsetAsync(bounds, 0, 8, st));
+        FP_HIP(hipMemsetAsync(bounds + 2, 0xFF, 8, st));
+        k_key_bounds<<<grid_for((SC + 3) / 4, 256) < 2048 ? grid_for((SC + 3) / 4, 256) : 2048, 256, 0, st>>>(
+            b->cpu_m, b->mem_mib, SC, bounds);
+        FP_HIP(hipGetLastError());
+        FP_HIP(hipMemcpyAsync(c->h_small, bounds, 16, hipMemcpyDeviceToHost, st));
         FP_HIP(hipStreamSynchronize(st));
-        const uint32_t dc = ((uint32_t *)c->h_small)[0], dm = ((uint32_t *)c->h_small)[1];
+        maxc = hs[0]; maxm = hs[1]; minc = hs[2]; minm = hs[3];
+    }
+    uint32_t cbits = fp_bitwidth(maxc), mbits = fp_bitwidth(maxm);
+    // dense ranks as key fields (a nonzero key only)
+    const uint32_t *bmc = nullptr, *bmm = nullptr, *prc = nullptr, *prm = nullptr;
+    const uint32_t *cval = nullptr, *mval = nullptr;
+    if (ranks && cbits + mbits > 0) {
         if (dc == 0 || dm == 0) return FP_EDEVICE;  // SC > 0: at least one value each
         bmc = rbm; bmm = rbm + RANK_WORDS; prc = rpre; prm = rpre + RANK_WORDS;
         cval = rval; mval = rval + RANK_MAX_VALUE;
