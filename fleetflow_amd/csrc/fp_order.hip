@@ -183,7 +183,7 @@ constexpr uint32_t kShards = 8;           // queues (blocks b and b+8 share an X
 constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B lines)
 constexpr uint64_t kQEmpty = ~0ull;
 constexpr uint32_t kCoopEdges = 16;       // edges left at which the wave expands a vertex together
-constexpr uint32_t kLaneEdges = 2;        // edges a lane relaxes per round
+constexpr uint32_t kLaneEdges = 1;        // edges a lane relaxes per round
 // ctl layout (u32 index): head[s] = s*32, tail[s] = (8+s)*32, done[s] = (16+s)*32,
 // fin = 24*32, abort = 25*32, maxlvl = 26*32
 constexpr uint32_t kCtlWords = 27 * kCtlStride;
@@ -202,7 +202,8 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // at level NONE (a source without out-edges is final here).
 __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
                                  const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t *__restrict__ level,
-                                 uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl) {
+                                 uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
+                                 bool pk) {
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = v < V;
     uint32_t l0 = 0, deg = 0;
@@ -222,13 +223,15 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(&ctl[(kShards + sh) * kCtlStride], (uint32_t)__popcll(m));
     base = __shfl(base, (int)leader);
-    if (push) Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)l0 << 32) | v;
+    if (push)
+        Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
+            ((uint64_t)(pk ? l0 << 8 : l0) << 32) | v;
 }
 
 __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
                                                   uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
                                                   uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
-                                                  uint32_t *__restrict__ err) {
+                                                  uint32_t *__restrict__ err, bool pk) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sh = blockIdx.x % kShards;
     uint32_t *head = &ctl[sh * kCtlStride];
@@ -242,18 +245,18 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
     // and at most one continuation cw (level cl, edges [ce, ce1) prefetched)
     bool has_claim = false, has_item = false;
     uint32_t slot = 0, u = 0, lu = 0, e = 0, e1 = 0, my_max = 0, idle = 0;
-    uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0;
+    uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0, eb = 0;  // eb: first edge of u
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     // deferred pushes (see below): entries, offsets, the reserved base (lane 0)
-    bool pend[kLaneEdges];
-    uint32_t pofs[kLaneEdges], pbase = 0, npend = 0;
-    uint64_t pent[kLaneEdges];
+    bool pend[kLaneEdges + 1];
+    uint32_t pofs[kLaneEdges + 1], pbase = 0, npend = 0;
+    uint64_t pent[kLaneEdges + 1];
     uint64_t *pq = Q;
     while (true) {
         if (npend) {
             const uint32_t base = __shfl(pbase, 0);
 #pragma unroll
-            for (uint32_t k = 0; k < kLaneEdges; ++k)
+            for (uint32_t k = 0; k <= kLaneEdges; ++k)
                 if (pend[k]) __hip_atomic_store(&pq[base + pofs[k]], pent[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             npend = 0;
         }
@@ -299,15 +302,17 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                     b0 = __shfl(b0, (int)leader);
                     if (rdy)
                         __hip_atomic_store(&Q[(size_t)ps * V + b0 + (uint32_t)__popcll(rm & lt)],
-                                           (cur & 0xFFFFFFFF00000000ull) | ww, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                                           ((uint64_t)(pk ? (uint32_t)(cur >> 32) << 8 : (uint32_t)(cur >> 32)) << 32) |
+                                               ww,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             if (lane == L) e = e1;  // the step below finishes (or continues) the item
         }
         // per-lane step: up to kLaneEdges edges at once (loads and first CAS attempts all in
         // flight together), so a chain link with a few fan-out children still takes one round
-        bool ready[kLaneEdges], fin_item = false;
+        bool ready[kLaneEdges], fin_item = false, part = false;
+        uint64_t pent_part = 0;
         uint32_t w[kLaneEdges], wl[kLaneEdges];
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k) ready[k] = false;
@@ -358,9 +363,16 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                 }
             }
             e += ne;
+            // a continuation with edges of u left: hand those to the queue as a partial
+            // item (entry level << 8 | edges to skip) and follow the chain now
+            if (cw != FP_NONE && e < e1 && pk && e - eb < 256u) {
+                part = true;
+                pent_part = ((uint64_t)((lu << 8) | (e - eb)) << 32) | u;
+                e = e1;
+            }
             if (e >= e1) {
                 if (cw != FP_NONE) {  // continue down the chain in this lane
-                    u = cw; lu = cl; e = ce; e1 = ce1;
+                    u = cw; lu = cl; e = ce; e1 = ce1; eb = ce;
                     cw = FP_NONE;
                     level[u] = lu;
                     my_max = max(my_max, lu);
@@ -374,8 +386,10 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             has_claim = false;
             has_item = true;
             u = (uint32_t)x;
-            lu = (uint32_t)(x >> 32);
-            e = row_ptr[u];
+            const uint32_t hi = (uint32_t)(x >> 32);
+            lu = pk ? hi >> 8 : hi;
+            eb = row_ptr[u];
+            e = eb + (pk ? (hi & 255u) : 0u);
             e1 = row_ptr[u + 1];
             level[u] = lu;
             my_max = max(my_max, lu);
@@ -399,23 +413,25 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         // pushes, deferred by one round: this round reserves the queue slots (the add's
         // result is not waited for), the next round stores the entries -- the reservation's
         // round trip overlaps the next round's loads instead of adding to this one
-        uint64_t rm[kLaneEdges];
+        uint64_t rm[kLaneEdges + 1];
         uint32_t tot = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k) {
             rm[k] = __ballot(ready[k]);
             tot += (uint32_t)__popcll(rm[k]);
         }
+        rm[kLaneEdges] = __ballot(part);
+        tot += (uint32_t)__popcll(rm[kLaneEdges]);
         if (tot) {
             const uint32_t ps = (sh + ++rr) % kShards;
             if (lane == 0) pbase = atomicAdd(&ctl[(kShards + ps) * kCtlStride], tot);
             pq = Q + (size_t)ps * V;
             uint32_t run = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < kLaneEdges; ++k) {
-                pend[k] = ready[k];
+            for (uint32_t k = 0; k <= kLaneEdges; ++k) {
+                pend[k] = k < kLaneEdges ? ready[k] : part;
                 pofs[k] = run + (uint32_t)__popcll(rm[k] & lt);
-                pent[k] = ((uint64_t)wl[k] << 32) | w[k];
+                pent[k] = k < kLaneEdges ? ((uint64_t)(pk ? wl[k] << 8 : wl[k]) << 32) | w[k] : pent_part;
                 run += (uint32_t)__popcll(rm[k]);
             }
             npend = 1;
@@ -558,14 +574,17 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         if (!state || !Q || !actl) return FP_ENOMEM;
         FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
         FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
-        k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl);
+        // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
+        const bool pk = V < (1u << 24);
+        k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl,
+                                                             pk);
         FP_HIP(hipGetLastError());
         FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
         FP_HIP(hipStreamSynchronize(st));
         if (((uint32_t *)c->h_small)[0]) return -(int)((uint32_t *)c->h_small)[0];
         if (E) {
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
-            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, g->col, V, state, Q, actl, level, c->d_err);
+            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, g->col, V, state, Q, actl, level, c->d_err, pk);
             FP_HIP(hipGetLastError());
         }
         FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
