@@ -15,7 +15,7 @@ constexpr int kPer = 4;       // containers per thread: one LDS node read serves
 constexpr int kTile = 1024;   // nodes per LDS chunk
 
 struct alignas(16) NodeRec {
-    uint32_t cf, mf, lab, cu;
+    uint32_t cf, mf, lab, cu;  // lab holds ~labels in the LDS tile
 };
 
 struct FeasArgs {
@@ -30,26 +30,29 @@ struct FeasArgs {
 
 // Block = 256 threads x kPer containers: container c = blockIdx.x * 1024 + k * 256 + threadIdx.x,
 // so each of a wave's kPer container words is one bitmap row.
+// Per (node, container) the test is two compares and ((req & ~lab) | (cu & conf)) == 0 with
+// ~lab staged in LDS; unschedulable nodes are skipped with a wave-uniform branch and absent
+// lanes are masked once (their count and first are never written), not per evaluation.
 __global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
-    __shared__ NodeRec rec[kTile];
+    __shared__ NodeRec rec[kTile];   // cf, mf, ~lab, cu
     __shared__ uint32_t sch[kTile];
     const uint32_t lane = threadIdx.x & 63;
     uint32_t cpu[kPer], mem[kPer], req[kPer], conf[kPer], first[kPer], cnt[kPer], cidx[kPer];
-    uint64_t word[kPer];
+    uint64_t word[kPer], cinm[kPer];
     bool cin[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const uint32_t c = blockIdx.x * (kBlock * kPer) + k * kBlock + threadIdx.x;
         cidx[k] = c;
         cin[k] = c < a.C;
-        // absent lanes get an impossible demand (never fits: cpu > any free cpu)
         cpu[k] = cin[k] ? a.cpu[c] : 0xFFFFFFFFu;
         mem[k] = cin[k] ? a.mem[c] : 0xFFFFFFFFu;
-        req[k] = cin[k] ? a.req[c] : 0u;
-        conf[k] = cin[k] ? a.conf[c] : 0u;
+        req[k] = cin[k] ? a.req[c] : 0xFFFFFFFFu;
+        conf[k] = cin[k] ? a.conf[c] : 0xFFFFFFFFu;
         first[k] = FP_NONE;
         cnt[k] = 0;
         word[k] = 0;
+        cinm[k] = __builtin_amdgcn_ballot_w64(cin[k]);  // absent lanes never set a bitmap bit
     }
     const uint32_t y0 = blockIdx.y * a.node_span;
     const uint32_t y1 = min(a.N, y0 + a.node_span);
@@ -57,23 +60,24 @@ __global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
         const uint32_t len = min((uint32_t)kTile, y1 - n0);
         for (uint32_t i = threadIdx.x; i < len; i += kBlock) {
             NodeRec r;
-            r.cf = a.cf[n0 + i]; r.mf = a.mf[n0 + i]; r.lab = a.lab[n0 + i]; r.cu = a.cu[n0 + i];
+            r.cf = a.cf[n0 + i]; r.mf = a.mf[n0 + i]; r.lab = ~a.lab[n0 + i]; r.cu = a.cu[n0 + i];
             rec[i] = r;
             sch[i] = a.sched[n0 + i];
         }
         __syncthreads();
         for (uint32_t i = 0; i < len; ++i) {
-            const NodeRec r = rec[i];
-            const bool sc = sch[i] != 0u;
             const uint32_t n = n0 + i;
+            if (__builtin_amdgcn_readfirstlane(sch[i])) {
+                const NodeRec r = rec[i];
 #pragma unroll
-            for (int k = 0; k < kPer; ++k) {
-                const bool ok = sc & cin[k] & fpd::fits(cpu[k], mem[k], req[k], conf[k], r.cf, r.mf, r.lab, r.cu);
-                cnt[k] += ok ? 1u : 0u;
-                first[k] = min(first[k], ok ? n : FP_NONE);
-                if (a.bitmap) {
-                    const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
-                    word[k] = lane == (i & 63) ? m : word[k];
+                for (int k = 0; k < kPer; ++k) {
+                    const bool ok = (r.cf >= cpu[k]) & (r.mf >= mem[k]) & (((req[k] & r.lab) | (r.cu & conf[k])) == 0u);
+                    cnt[k] += ok ? 1u : 0u;
+                    first[k] = min(first[k], ok ? n : FP_NONE);
+                    if (a.bitmap) {
+                        const uint64_t m = __builtin_amdgcn_ballot_w64(ok) & cinm[k];  // every lane takes part
+                        word[k] = lane == (i & 63) ? m : word[k];
+                    }
                 }
             }
             if (a.bitmap && ((i & 63) == 63 || i + 1 == len)) {
@@ -82,6 +86,7 @@ __global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
                 for (int k = 0; k < kPer; ++k) {
                     const uint32_t wword = (blockIdx.x * (kBlock * kPer) + k * kBlock + (threadIdx.x & ~63u)) / 64;
                     if (lane <= (i & 63) && wword < a.WC) a.bitmap[(size_t)wword * a.N + nb + lane] = word[k];
+                    word[k] = 0;  // skipped (unschedulable) nodes of the next 64 stay zero
                 }
             }
         }
