@@ -270,7 +270,6 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     const unsigned long long ck_t0 = STAT_CLK();
     unsigned long long ck_a, ck_b;
     bool alive = true;
-
     while (alive) {
         ck_a = STAT_CLK();
         uint32_t cpu = 0, mem = 0, req = 0, conf = 0, idx = 0;
@@ -801,6 +800,11 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     uint32_t R = 2;
     for (uint32_t r = 4; r > 2; --r)
         if (lds_bytes(W, G, r) <= LDS_HALF_CU) { R = r; break; }
+    // FLEETPLACE_PIPE_R: force the ring depth, 2..6 (a link's control block holds 6 slot counts)
+    if (getenv("FLEETPLACE_PIPE_R")) {
+        const int fr = atoi(getenv("FLEETPLACE_PIPE_R"));
+        if (fr >= 2 && fr <= 6 && lds_bytes(W, G, (uint32_t)fr) <= 160 * 1024) R = (uint32_t)fr;
+    }
     lds = lds_bytes(W, G, R);
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;

@@ -333,6 +333,19 @@ def test_ffd_sort_key_compression(case, planner, O):
         assert np.array_equal(reason[s * C:(s + 1) * C], er)
 
 
+def test_ffd_sort_rank_keys_u64(planner, O):
+    """~140k distinct cpu and mem values below 2^18: the rank fields need 18 + 18 bits, so
+    the rank keys go to the u64 sort (fp_place.hip); the plan must still be the oracle's."""
+    rng = np.random.default_rng(11)
+    C, N = 140_000, 300
+    cpu = rng.permutation(1 << 18)[:C].astype(np.uint32)
+    mem = rng.permutation(1 << 18)[:C].astype(np.uint32)
+    cont = (cpu, mem, np.zeros(C, np.uint32), np.zeros(C, np.uint32))
+    nodes = (rng.integers(1 << 18, 1 << 22, N).astype(np.uint32), rng.integers(1 << 18, 1 << 22, N).astype(np.uint32),
+             np.zeros(N, np.uint32), np.zeros(N, np.uint32), np.ones(N, np.uint8))
+    _check_ffd(planner, O, cont, nodes)
+
+
 # ---- segmented pipeline: N beyond one workgroup's LDS (> 80 groups of 64 nodes) ----
 @pytest.mark.parametrize("C,N,flags", [(20_000, 6_000, 7), (30_000, 20_000, 7), (2_000, 100_000, 7),
                                        (60_000, 33_000, 3), (5_000, 5_121, 7)])
