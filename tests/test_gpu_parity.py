@@ -97,6 +97,23 @@ def test_levelize_async_shapes(shape, planner, O):
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
+def test_levelize_async_unpacked_entries(planner, O):
+    """V >= 2^24: queue entries cannot pack (level << 8 | skip), so the asynchronous
+    levelizer runs without partial hand-off (fp_order.hip `pk`); same levels and order."""
+    rng = np.random.default_rng(3)
+    V = (1 << 24) + 100
+    heads = rng.integers(0, V - 600, 40)
+    edges = [(int(h) + i, int(h) + i + 1) for h in heads for i in range(500)]
+    edges += [(int(h), int(t)) for h, t in zip(rng.integers(0, V, 3000), rng.integers(0, V, 3000)) if h < t]
+    edges = sorted(set(edges))
+    rp, col = _csr(V, edges)
+    hd = np.zeros(V, np.uint8)
+    hd[np.unique(col)] = 1
+    level, order, ncyc = planner.levelize(rp, col, hd)
+    el, eo, en = O.levelize(rp, col, hd)
+    assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
 def test_levelize_config5_full_size(planner, O):
     """BASELINE config 5: 1M vertices (1000 chains x 500 + 50 layers x 10k), 333 3-cycles."""
     rp, col, hd = O.gen_dag(SEED + 5, 1000, 500, 50, 10_000, 333)
