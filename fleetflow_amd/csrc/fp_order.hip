@@ -3,9 +3,11 @@
 //  * fp_dev_legacy_order: crates/fleetflow-container/src/engine.rs:67-85 as a stable
 //    two-bucket partition (has_deps == 0 first, each bucket in input order),
 //    computed with wavefront ballots + a block-offset scan.
-//  * fp_dev_levelize: SPEC.md 2.2, frontier-parallel Kahn over the reversed CSR.
-//    level(v) = max(has_deps(v), max_{d->v} level(d)+1) is unique, so the frontier
-//    schedule (atomic order inside a level) cannot change the result.
+//  * fp_dev_levelize: SPEC.md 2.2, Kahn over the reversed CSR, asynchronous by default
+//    (k_lvl_async: a persistent grid on sharded work queues, no per-level launch;
+//    DESIGN.md 4.4), level-synchronous with FLEETPLACE_LEVELIZE=levels (one k_expand
+//    launch per level).  level(v) = max(has_deps(v), max_{d->v} level(d)+1) is unique,
+//    so neither schedule (nor the atomic order inside it) can change the result.
 #include "fp_internal.h"
 #include <rocprim/device/device_radix_sort.hpp>
 #include <stdlib.h>
