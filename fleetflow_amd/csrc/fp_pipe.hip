@@ -60,6 +60,9 @@ constexpr uint32_t CYC = 0x80000000u;
 // launch, so the bound is wall-clock time, not an iteration count.
 constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s
 constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per group)
+#ifndef FP_SPIN_MAX
+#define FP_SPIN_MAX 12              // longest back-off sleep of an idle stage (x 64 cycles)
+#endif
 constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
 
 struct PipeArgs {
@@ -125,7 +128,7 @@ __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_
         // back off: a spinning wave still takes issue slots from its CU's busy waves
         if (n < 8) __builtin_amdgcn_s_sleep(1);
         else if (n < 32) __builtin_amdgcn_s_sleep(4);
-        else __builtin_amdgcn_s_sleep(12);
+        else __builtin_amdgcn_s_sleep(FP_SPIN_MAX);
     }
 }
 
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                     }
                 }
                 if (n_sp < 8) __builtin_amdgcn_s_sleep(2);
-                else __builtin_amdgcn_s_sleep(12);
+                else __builtin_amdgcn_s_sleep(FP_SPIN_MAX);
             }
             st_spin_in += n_sp;
             if (!got) break;
