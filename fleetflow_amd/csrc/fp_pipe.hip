@@ -405,6 +405,40 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
         } else
 #endif
+        if constexpr (G == 1) {
+            // one-group stages (few scenarios): every todo container has exactly one
+            // candidate group, so one check each and no candidate bookkeeping
+            while (todo) {
+                const uint32_t ti = (uint32_t)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                const uint32_t c_cpu = __builtin_amdgcn_readlane(cpu, ti);
+                const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
+                const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
+                const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
+                const uint32_t x = rcf[0], y = rmf[0], z = rcu[0];
+                if (STAT_ON) st_checks++;
+                const uint64_t m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
+                                   __builtin_amdgcn_ballot_w64(((rlab[0] & c_req) | (z & c_conf)) == 0u);
+                if (m) {
+                    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                    const uint32_t oc = __builtin_amdgcn_readlane(x, l);
+                    const uint32_t om = __builtin_amdgcn_readlane(y, l);
+                    const uint32_t nc = oc - c_cpu, nm = om - c_mem;
+                    const bool me = lane == l;
+                    rcf[0] = me ? nc : x;
+                    rmf[0] = me ? nm : y;
+                    rcu[0] = me ? (z | c_conf) : z;
+                    usedbits |= me ? 1u : 0u;
+                    const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
+                    const bool crossed = (my_t <= ov) & (my_t > nv);
+                    atomicAnd((unsigned long long *)&Mw[(lane & (K - 1)) * 2 + (lane >> 5)],
+                              crossed ? ~(1ull << l) : ~0ull);
+                    placed |= 1ull << ti;
+                    my_assign = lane == ti ? gbase * 64 + l : my_assign;
+                    if (STAT_ON) st_hits++;
+                }
+            }
+        } else
         // Exact first fit, container by container in FFD order; group g's records are
         // read and written in registers through a wave-uniform index.
         {
