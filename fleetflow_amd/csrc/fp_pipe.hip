@@ -23,8 +23,9 @@
 // clearing bits on placement and a stale mask is always a superset: only
 // candidate groups get the exact check.
 #include "fp_internal.h"
-// 10-group stages (the wide geometry: configs 3, 4, 5) run the hand-scheduled candidate
-// loop of fp_pipe_asm.h; -DFP_NO_ASM builds the C++ loop everywhere (A/B, reference)
+// Stages of 2..10 groups (the wide geometry: config 4 and other many-scenario batches) run
+// the hand-scheduled candidate loop of fp_pipe_asm.h, one-group stages (configs 2, 3, 5) a
+// specialised C++ loop; -DFP_NO_ASM builds the C++ loops everywhere (A/B, reference)
 #ifndef FP_NO_ASM
 #define FP_ASM
 #endif
@@ -175,7 +176,7 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 // promoted, read and written through s_set_gpr_idx; a pinned tuple in the asm build)
 #ifdef FP_ASM
 template <uint32_t G>
-using RecT = typename std::conditional<G == 10, rec10, uint32_t[G]>::type;
+using RecT = typename std::conditional<(G >= 2 && G <= 10), rec10, uint32_t[G]>::type;
 #else
 template <uint32_t G>
 using RecT = uint32_t[G];
@@ -394,8 +395,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
 #endif
 #ifdef FP_ASM
         // Exact first fit, container by container in FFD order: the hand-scheduled
-        // loop (fp_pipe_asm.h) for 10-group stages.  Same algorithm as the C++ loop below.
-        if constexpr (G == 10) {
+        // loop (fp_pipe_asm.h) for 2..10-group stages.  Same algorithm as the C++ loop below.
+        if constexpr (G >= 2 && G <= 10) {
             const uint32_t lane_sel = lane < 32u ? 0xFFFFFFFFu : 0u;
             const uint32_t maddr = (uint32_t)(size_t)(__attribute__((address_space(3))) uint64_t *)(
                 Mw + (lane & (K - 1)) * 2 + (lane >> 5));

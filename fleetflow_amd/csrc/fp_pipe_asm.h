@@ -10,7 +10,7 @@
 //   * the bucket-mask update is one ds_mskor_b64 with no per-lane select of the old value.
 // gfx950 (GFX9 encoding): one SGPR per VALU op, lane selects come from SALU results or
 // M0, and M0 is reloaded after every s_set_gpr_idx window (the window overwrites it);
-// M0 is restored on exit (the compiler treats it as reserved).  Written for 10-group
+// M0 is restored on exit (the compiler treats it as reserved).  Written for 2..10-group
 // stages (the wide geometry): records v[88:127], scratch v[76:87], so the wave stays
 // within 128 VGPRs (four workgroups of four waves per CU).
 #pragma once
