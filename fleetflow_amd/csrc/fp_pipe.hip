@@ -689,7 +689,7 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const size_t i = i0 + (size_t)u * stride;
-            if (i < total) j[u] = order[i];
+            if (i < total) j[u] = __builtin_nontemporal_load(&order[i]);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -697,7 +697,7 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
             if (i < total) {
                 src[u] = (uint32_t)i - (uint32_t)i % C + j[u];  // i < total < 2^32
                 if (skeys) {
-                    const uint64_t k = skeys[i];
+                    const uint64_t k = __builtin_nontemporal_load(&skeys[i]);
                     cv[u] = (uint32_t)(cmax - (mbits >= 64 ? 0ull : ((k >> mbits) & cmax)));
                     mv[u] = (uint32_t)(mmax - (k & mmax));
                 }
@@ -723,11 +723,12 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
         for (int u = 0; u < 4; ++u) {
             const size_t i = i0 + (size_t)u * stride;
             if (i < total) {
-                s_cpu[i] = cv[u];
-                s_mem[i] = mv[u];
-                s_req[i] = r[u];
-                s_conf[i] = f[u];
-                s_idx[i] = j[u] | cy[u];
+                // streaming traffic bypasses L2 retention so the random req/conf lines stay
+                __builtin_nontemporal_store(cv[u], &s_cpu[i]);
+                __builtin_nontemporal_store(mv[u], &s_mem[i]);
+                __builtin_nontemporal_store(r[u], &s_req[i]);
+                __builtin_nontemporal_store(f[u], &s_conf[i]);
+                __builtin_nontemporal_store(j[u] | cy[u], &s_idx[i]);
             }
         }
     }
