@@ -515,8 +515,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         const uint32_t tl_idx = st_batches - 1;
 #endif
         if ((placed >> lane) & 1ull) {
-            __builtin_nontemporal_store(my_assign, &a.assign[cb + idx]);  // scattered, never re-read
-            __builtin_nontemporal_store((uint8_t)FP_REASON_OK, &a.reason[cb + idx]);
+            a.assign[cb + idx] = my_assign;
+            a.reason[cb + idx] = FP_REASON_OK;
         }
 #ifdef FP_PIPE_STATS
         if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B) {
@@ -552,8 +552,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         }
         if (!has_out) {
             if (fwd) {
-                __builtin_nontemporal_store((uint32_t)FP_NONE, &a.assign[cb + idx]);
-                __builtin_nontemporal_store((uint8_t)FP_REASON_NOFIT, &a.reason[cb + idx]);
+                a.assign[cb + idx] = FP_NONE;
+                a.reason[cb + idx] = FP_REASON_NOFIT;
             }
             n_rej += (uint32_t)__popcll(__ballot(fwd));
             continue;
