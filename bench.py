@@ -1,32 +1,55 @@
 """Benchmark: container x node evaluations/s for FFD what-if planning on MI355X.
 
-Workload (BASELINE.json configs[3], sharded weak): every rank plans S_LOCAL=512
-independent what-if scenarios of 50k containers x 5k nodes (SPEC.md section 3
-synthetic clusters, generated on the device), so --gpus 8 runs exactly config
-4's 4096 scenarios.  One step = restore the pristine node tables (D2D copy) +
-FFD plan of every local scenario (key sort + placement kernel + packed cost) +
-one all-gather of the packed costs over RCCL (N>1) + the global argmin.
+Headline workload = BASELINE.json configs[3] at its stated size: S = 4096 what-if
+scenarios of 50k containers x 5k nodes (ports + anti-affinity + labels, SPEC.md 3
+synthetic clusters generated on the device).  Strong scaling: the 4096 scenarios
+are split into contiguous blocks, rank r plans 4096/N of them, so N = 1 runs the
+whole config on one GPU and SCALE's N = 1 line equals BENCH.
 
-value = S_total * C * N / step_time  ("work-equivalent" evals: SURVEY.md 8(d)).
-roofline.achieved = 16 B x (S_local*C*N) / average FFD-kernel duration, measured
-with HIP events on the launch stream (16 B per container x node
-evaluation); peak = 8000 GB/s HBM (MI355X_MICROARCH.md).
+One step = restore the pristine node tables (D2D) + FFD plan of every local
+scenario (key sort + placement kernel + packed cost) + all-gather of the packed
+costs over RCCL (N > 1) + argmin + hand-off of the winning plan from its owner
+rank (one broadcast, N > 1; a D2D copy at N = 1).
+
+value = S_total * C * N / step_time ("work-equivalent" evals/s, SURVEY.md 8(d):
+the brute-force container x node count; the kernel prunes most of it).
+
+roofline (dominant kernel k_ffd_pipe): achieved = HBM bytes per launch measured
+with rocprofv3 PMC (FETCH_SIZE x 2 gfx950 correction + WRITE_SIZE, separate
+passes, profiles/pmc_latest.json) / the kernel's average duration, timed live with
+HIP events on the launch stream; peak 8000 GB/s.  The kernel is bound by the
+latency of the sequential first-fit chain, not by HBM: `latency_model` compares
+the measured time with checks x cycles-per-check from the diagnostics build
+(profiles/pipe_model_latest.json).  The 16 B x S*C*N figure is reported under
+`work_equivalent`, labelled as what it is.
+
+A second leg, `config3`, times BASELINE configs[2] (1 scenario x 1M containers x
+100k nodes, the north-star sweep) on rank 0 at N = 1.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+--gpus N without an external launcher starts N worker processes itself (before
+any GPU call in this parent), one per GPU, over torch.distributed (RCCL).
 """
 import argparse
 import json
+import math
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-C_PER_SCEN = 50_000
-N_PER_SCEN = 5_000
-S_LOCAL = 512
-SEED = 0x5EED0004
+C4, N4, S4, SEED4 = 50_000, 5_000, 4096, 0x5EED0004
+C3, N3, SEED3 = 1_000_000, 100_000, 0x5EED0003
 FLAGS = 7
 HBM_PEAK_GBPS = 8000.0
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
+MODEL_FILE = os.path.join(ROOT, "profiles", "pipe_model_latest.json")
 
 
 def parse():
@@ -34,166 +57,316 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scenarios-per-gpu", type=int, default=S_LOCAL)
-    ap.add_argument("--cpu-budget-s", type=float, default=15.0, help="CPU baseline sample budget (wall s)")
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
-                    help="host threads for the CPU baseline (the GPU box grants 16 per GPU)")
+    ap.add_argument("--scenarios", type=int, default=S4, help="total what-if scenarios (config 4: 4096)")
+    ap.add_argument("--config3-steps", type=int, default=3)
+    ap.add_argument("--no-config3", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0, help="CPU baseline sample budget (wall s)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads for the CPU baseline (default: min(16, usable cores); the GPU box grants 16/GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="test hook: each rank prints its rank/world env as JSON and exits (no GPU call)")
     return ap.parse_args()
 
 
+# ---------------------------------------------------------------------------------------------
+# launcher: `python bench.py --gpus N` without torchrun starts N ranks (this parent never
+# initialises HIP; each child is a fresh process that binds its own GPU)
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        rc = rc or code
+    return rc
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the oracle FFD on whole config-4 scenarios
+# ---------------------------------------------------------------------------------------------
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(budget_s, threads):
-    """Oracle FFD (oracle/fp_oracle.c) on a bounded sample of the same workload:
-    whole scenarios of rank 0's shard, one per host thread at a time (the C calls
-    release the GIL), until ~budget_s of wall time.  Also reports the
-    single-thread rate measured on the first scenario."""
+    """oracle/fp_oracle.c fpo_place (sort + first-fit scan) on whole 50k x 5k scenarios of
+    the same workload, `threads` scenarios at a time on as many host threads (ctypes drops
+    the GIL).  1 warm-up wave, then timed waves until ~budget_s (at least 5); the value is
+    the median wave rate.  Inputs are generated before the timed waves."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O  # the checker, timed as the CPU baseline only
     O.lib()
-    inputs = [O.gen_scenario(SEED, s, C_PER_SCEN, N_PER_SCEN, FLAGS) for s in range(threads)]
-    t0 = time.perf_counter()
-    O.place(*inputs[0])
-    single = C_PER_SCEN * N_PER_SCEN / (time.perf_counter() - t0)
-
-    def one(s):
-        cont, nodes = inputs[s % threads] if s < threads else O.gen_scenario(SEED, s, C_PER_SCEN, N_PER_SCEN, FLAGS)
-        O.place(cont, nodes)
-
-    done = 0
-    t0 = time.perf_counter()
+    inputs = [O.gen_scenario(SEED4, s, C4, N4, FLAGS) for s in range(threads)]
+    singles = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        O.place(*inputs[0])
+        singles.append(C4 * N4 / (time.perf_counter() - t0))
+    rates = []
     with ThreadPoolExecutor(threads) as ex:
-        while time.perf_counter() - t0 < budget_s and done < S_LOCAL:
-            n = min(threads, S_LOCAL - done)
-            list(ex.map(one, range(done, done + n)))
-            done += n
-    wall = time.perf_counter() - t0
-    return {"value": done * C_PER_SCEN * N_PER_SCEN / wall, "unit": "evals/s", "cores": threads, "kind": "port",
-            "single_thread_value": single,
-            "sample": f"{done} whole scenarios of 50k x 5k, {threads} at a time on {threads} host threads "
-                      f"(oracle/fp_oracle.c fpo_place: sort + first-fit scan), {wall:.1f} s wall"}
-
-
-def load_traffic():
-    """HBM bytes per FFD launch from the committed rocprofv3 --pmc summary, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_ffd_latest.json")
-    if not os.path.exists(p):
-        return None
+        list(ex.map(lambda i: O.place(*inputs[i]), range(threads)))  # warm-up wave
+        t_start = time.perf_counter()
+        while len(rates) < 5 or time.perf_counter() - t_start < budget_s:
+            t0 = time.perf_counter()
+            list(ex.map(lambda i: O.place(*inputs[i]), range(threads)))
+            rates.append(threads * C4 * N4 / (time.perf_counter() - t0))
+            if len(rates) >= 200:
+                break
+        wall = time.perf_counter() - t_start
     try:
-        with open(p) as f:
-            d = json.load(f)
-        if d.get("scenarios_per_launch") == S_LOCAL and d.get("C") == C_PER_SCEN and d.get("N") == N_PER_SCEN:
-            return d.get("hbm_bytes_per_launch")
-    except Exception:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"value": statistics.median(rates), "unit": "evals/s", "cores": threads, "kind": "port",
+            "single_thread_value": statistics.median(singles),
+            "nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": _cpu_model(),
+            "sample": f"{len(rates)} waves of {threads} whole 50k x 5k config-4 scenarios on {threads} host "
+                      f"threads (oracle/fp_oracle.c fpo_place: sort + first-fit scan), median wave rate, "
+                      f"{wall:.1f} s timed after 1 warm-up wave; single-thread = median of 3 scenarios"}
+
+
+# ---------------------------------------------------------------------------------------------
+# roofline helpers
+# ---------------------------------------------------------------------------------------------
+def _load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
         return None
-    return None
 
 
-def main():
-    args = parse()
+def pmc_record(leg, S, C, N):
+    """PMC HBM bytes of one k_ffd_pipe launch for this leg, from the committed rocprofv3
+    summary (profiles/pmc_latest.json, tools/pmc_summary.py).  Scaled per scenario when
+    only the per-scenario count differs (strong-scaled ranks)."""
+    d = _load_json(PMC_FILE)
+    rec = (d or {}).get(leg)
+    if not rec or rec.get("C") != C or rec.get("N") != N:
+        return None, None
+    b = rec["hbm_bytes_per_launch"]
+    if rec.get("S") != S:
+        b = b / rec["S"] * S
+    return b, rec
+
+
+def roofline(leg, S, C, N, kernel_s, step_s):
+    traffic, rec = pmc_record(leg, S, C, N)
+    achieved = traffic / kernel_s / 1e9 if traffic else None
+    ess = S * (C * 21 + N * 29)  # containers in (16 B) + out (5 B); nodes in (17 B) + back (12 B)
+    out = {"bound": "hbm", "limiter": "latency of the sequential first-fit chain (see latency_model)",
+           "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBPS if achieved else None, "traffic": traffic,
+           "traffic_source": (f"rocprofv3 PMC {rec.get('tag')}: 2 x FETCH_SIZE + WRITE_SIZE per launch, "
+                              f"separate passes (profiles/pmc_latest.json)") if rec else None,
+           "kernel": "k_ffd_pipe (fleetflow_amd/csrc/fp_pipe.hip)", "kernel_ms": kernel_s * 1e3,
+           "essential_bytes": ess, "essential_GBps": ess / kernel_s / 1e9,
+           "work_equivalent": {"note": "16 B x S*C*N brute-force evaluations / kernel time: a work count, "
+                                       "NOT bandwidth (pruned evaluations never touch memory)",
+                               "evals_per_launch": S * C * N,
+                               "GBps": 16 * S * C * N / kernel_s / 1e9}}
+    m = (_load_json(MODEL_FILE) or {}).get(leg)
+    if m and m.get("C") == C and m.get("N") == N:
+        rounds = math.ceil(S / m["resident_scenarios"])
+        model_ms = rounds * m["chain_cycles_per_scenario"] / (m["clock_ghz"] * 1e6)
+        out["latency_model"] = dict(m, rounds=rounds, model_ms=model_ms, measured_kernel_ms=kernel_s * 1e3,
+                                    formula="ceil(S / resident_scenarios) x chain_cycles_per_scenario / clock")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# workers
+# ---------------------------------------------------------------------------------------------
+def timed(steps, step, sync, barrier):
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def config3_leg(planner, dev, steps, warmup):
+    """BASELINE configs[2]: 1 x 1M containers x 100k nodes, flags 7 (a replica per GPU)."""
+    import torch
+
+    from fleetflow_amd import DevBatch
+    from fleetflow_amd._lib import FP_K_PLACE, FP_K_SORT
+    db = DevBatch.allocate(1, C3, N3, dev)
+    planner.dev_gen_batch(SEED3, db, FLAGS)
+    pristine = db.node_snapshot()
+
+    def step():
+        db.restore_nodes(pristine)
+        planner.dev_place_batch(db)
+
+    for _ in range(max(1, warmup)):
+        step()
+    torch.cuda.synchronize(dev)
+    ref = db.assign.clone()
+    planner.profile(True)
+    el = timed(steps, step, lambda: torch.cuda.synchronize(dev), lambda: None)
+    planner.sync()
+    if not torch.equal(db.assign, ref):
+        raise RuntimeError("config 3: timed steps did not reproduce the warmup plan")
+    k_ms, k_n = planner.kernel_stats(FP_K_PLACE)
+    s_ms, s_n = planner.kernel_stats(FP_K_SORT)
+    planner.profile(False)
+    step_s = el / steps
+    kernel_s = k_ms / max(k_n, 1) / 1e3
+    placed = int((db.reason == 0).sum().item())
+    out = {"workload": "BASELINE config 3: 1 scenario x 1M containers x 100k nodes, ports+anti-affinity+labels",
+           "value": C3 * N3 / step_s, "unit": "evals/s (work-equivalent)", "ms_per_step": step_s * 1e3,
+           "steps": steps, "placed": placed, "nofit": C3 - placed,
+           "breakdown_ms": {"ffd_kernel": kernel_s * 1e3, "sort": s_ms / max(s_n, 1)},
+           "ns_per_container": step_s / C3 * 1e9,
+           "roofline": roofline("config3", 1, C3, N3, kernel_s, step_s)}
+    del db, pristine
+    torch.cuda.empty_cache()
+    return out
+
+
+def worker(args):
+    if args.dry_launch:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "MASTER_PORT")}), flush=True)
+        return
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
 
     from fleetflow_amd import DevBatch, Planner, shard
     from fleetflow_amd._lib import FP_K_PLACE, FP_K_SORT
 
-    S = args.scenarios_per_gpu
-    C, N = C_PER_SCEN, N_PER_SCEN
+    S_total, C, N = args.scenarios, C4, N4
+    shard.check_scenario_ids(S_total)
+    base, S = shard.block(rank, world, S_total)
     planner = Planner(local_rank)
     # one dedicated stream for torch's copies/collectives AND the planner kernels
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     planner.set_stream(stream.cuda_stream)
-    base, _ = shard.block(rank, world, S * world)
     db = DevBatch.allocate(S, C, N, dev, scen_base=base)
-    planner.dev_gen_batch(SEED, db, FLAGS)
+    planner.dev_gen_batch(SEED4, db, FLAGS)
     pristine = db.node_snapshot()
     best = torch.empty(1, dtype=torch.int32, device=dev)
+    plan = torch.empty(shard.plan_words(C), dtype=torch.int32, device=dev)
+    winner = {}
 
     def step():
         db.restore_nodes(pristine)
         planner.dev_place_batch(db)
-        if world > 1:
-            planner.dev_argmin_cost(shard.gather_costs(db.cost, world, S * world), best)
-        else:
-            planner.dev_argmin_cost(db.cost, best)
+        costs = shard.gather_costs(db.cost, world, S_total) if world > 1 else db.cost
+        planner.dev_argmin_cost(costs, best)
+        b = int(best.item())  # every rank holds the same winner
+        winner["best"] = b
+        winner["owner"] = shard.hand_off_plan(b, db.assign, db.reason, C, rank, world, S_total, plan)
 
+    barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
-    ref_cost = db.cost.clone()
-    ref_assign_sum = int(db.assign.sum().item())
+    ref_cost, ref_plan = db.cost.clone(), plan.clone()
     planner.profile(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(args.steps, step, lambda: torch.cuda.synchronize(dev), barrier)
+    planner.sync()  # raises on a sticky kernel error (e.g. the pipeline's deadlock guard)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     # every timed step re-planned the same inputs: its plans must be bit-identical
-    if not torch.equal(db.cost, ref_cost) or int(db.assign.sum().item()) != ref_assign_sum:
+    if not torch.equal(db.cost, ref_cost) or not torch.equal(plan, ref_plan):
         raise RuntimeError("timed steps did not reproduce the warmup plan (stream ordering bug?)")
     place_ms, place_n = planner.kernel_stats(FP_K_PLACE)
     sort_ms, sort_n = planner.kernel_stats(FP_K_SORT)
-    best_id = int(best.item())
+    planner.profile(False)
+    # per-rank kernel time, max over ranks (the slowest rank sets the step)
+    kt = torch.tensor([place_ms / max(place_n, 1), sort_ms / max(sort_n, 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+    kernel_ms, sort_avg_ms = float(kt[0].item()), float(kt[1].item())
 
+    out = None
     if rank == 0:
-        evals_total = S * world * C * N
         step_s = elapsed / args.steps
-        kernel_s = (place_ms / max(place_n, 1)) / 1e3
-        evals_launch = S * C * N
-        achieved = evals_launch * 16 / kernel_s / 1e9
-        traffic = load_traffic()
         out = {
             "metric": "container x node evaluations/sec (FFD what-if plans, work-equivalent) "
                       "+ achieved GB/s % HBM roofline",
-            "value": evals_total / step_s,
+            "value": S_total * C * N / step_s,
             "unit": "evals/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": step_s * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (SPEC.md 3, SplitMix64 seed 0x5EED0004, generated on device)",
-            "config": {"workload": "BASELINE config 4: what-if FFD, 512 scenarios/GPU x 50k containers x 5k "
-                                   "nodes, ports+anti-affinity+labels, RCCL all-gather of packed costs + argmin",
-                       "scenarios_per_gpu": S, "scenarios_total": S * world, "containers": C, "nodes": N,
+            "config": {"workload": f"BASELINE config 4: {S_total} what-if scenarios x 50k containers x 5k nodes, "
+                                   "ports+anti-affinity+labels; RCCL all-gather of packed costs + argmin + "
+                                   "winner plan broadcast from its owner",
+                       "scenarios_total": S_total, "scenarios_per_gpu": S, "containers": C, "nodes": N,
                        "parallelism": f"scenario-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "traffic_GBps": (traffic / kernel_s / 1e9) if traffic else None,
-                         "kernel": "k_ffd_pipe (fp_pipe.hip)", "kernel_ms": kernel_s * 1e3,
-                         "units_per_launch": evals_launch, "bytes_per_unit": 16},
-            "breakdown_ms": {"ffd_kernel": place_ms / max(place_n, 1), "sort": sort_ms / max(sort_n, 1)},
-            "best_scenario": best_id,
+            "roofline": roofline("config4", S, C, N, kernel_ms / 1e3, step_s),
+            "breakdown_ms": {"ffd_kernel": kernel_ms, "sort": sort_avg_ms},
+            "best_scenario": winner["best"], "best_owner_rank": winner["owner"],
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_budget_s, args.cpu_threads)
+    # the config-3 leg and the CPU baseline only at N = 1 (single-scenario replicas do not shard)
+    if world == 1 and rank == 0:
+        del db, pristine
+        torch.cuda.empty_cache()
+        if not args.no_config3:
+            out["config3"] = config3_leg(planner, dev, args.config3_steps, 1)
+        if not args.no_cpu_baseline:
+            try:
+                usable = len(os.sched_getaffinity(0))
+            except AttributeError:
+                usable = os.cpu_count() or 1
+            threads = args.cpu_threads or min(16, usable)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_budget_s, threads)
+    if out is not None:
         print(json.dumps(out), flush=True)
     planner.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    worker(args)
 
 
 if __name__ == "__main__":

@@ -46,6 +46,10 @@ extern "C" int fp_ctx_create(fp_ctx **out, int device) {
         fp_ctx_destroy(c);
         return FP_EDEVICE;
     }
+    if (hipMemset(c->d_err, 0, 256) != hipSuccess) {
+        fp_ctx_destroy(c);
+        return FP_EDEVICE;
+    }
     c->stream = c->own_stream;
     *out = c;
     return FP_OK;
@@ -61,27 +65,33 @@ extern "C" void fp_ctx_destroy(fp_ctx *c) {
     if (c->stage) (void)hipFree(c->stage);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
 
+// Switching streams drains the old one first: the workspace arena is reset by every call,
+// so work still queued on the old stream must not overlap a call on the new one.
 extern "C" int fp_ctx_set_stream(fp_ctx *c, void *s) {
     if (!c) return FP_EINVAL;
+    if ((hipStream_t)s != c->stream) {
+        FP_HIP(hipSetDevice(c->device));
+        FP_HIP(hipStreamSynchronize(c->stream));
+    }
     c->stream = (hipStream_t)s;  // NULL = HIP null stream
     return FP_OK;
 }
 
 extern "C" int fp_ctx_reset_stream(fp_ctx *c) {
-    if (!c) return FP_EINVAL;
-    c->stream = c->own_stream;
-    return FP_OK;
+    return fp_ctx_set_stream(c, c ? (void *)c->own_stream : nullptr);
 }
 
+// Waits for every fp_dev_* call queued on the context's stream and reports the first
+// kernel-side error any of them raised since the last report (then clears it).
 extern "C" int fp_ctx_sync(fp_ctx *c) {
     if (!c) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    FP_HIP(hipStreamSynchronize(c->stream));
-    return FP_OK;
+    return fp_take_err(c);
 }
 
 // ---- arenas ----------------------------------------------------------------
@@ -124,12 +134,14 @@ void *fp_stage_take(fp_ctx *c, size_t bytes) {
     return c->stage + top;
 }
 
-int fp_check_err(fp_ctx *c) {
+int fp_take_err(fp_ctx *c) {
     FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     FP_HIP(hipStreamSynchronize(c->stream));
-    uint32_t e = (uint32_t)c->h_small[0];
-    if (e) return -(int)e;
-    return FP_OK;
+    const uint32_t e = ((const uint32_t *)c->h_small)[0];
+    if (!e) return FP_OK;
+    FP_HIP(hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    FP_HIP(hipStreamSynchronize(c->stream));
+    return -(int)e;
 }
 
 // ---- profiling ---------------------------------------------------------------
@@ -221,9 +233,40 @@ static T *stage_out(fp_ctx *c, size_t n, int *rc) {
     if (!d) *rc = FP_ENOMEM;
     return d;
 }
-static int copy_back(fp_ctx *c, void *h, const void *d, size_t bytes) {
-    if (!h || !bytes) return FP_OK;
-    FP_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
+// Results of a host-pointer call: every device buffer goes to pinned staging first; the
+// caller's buffers are written only after the kernels' error word and every copy came
+// back clean ("on error nothing is written", fleetplace.h).
+struct OutCopy {
+    void *h;
+    const void *d;
+    size_t bytes;
+};
+static int copy_back_all(fp_ctx *c, const OutCopy *o, int n) {
+    size_t total = 0;
+    for (int i = 0; i < n; ++i)
+        if (o[i].h && o[i].bytes) total += align256(o[i].bytes);
+    if (total > c->h_stage_cap) {
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_cap = 0;
+        const size_t cap = align256(total + total / 4 + 4096);
+        FP_HIP(hipHostMalloc(&c->h_stage, cap, hipHostMallocDefault));
+        c->h_stage_cap = cap;
+    }
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!o[i].h || !o[i].bytes) continue;
+        FP_HIP(hipMemcpyAsync(c->h_stage + off, o[i].d, o[i].bytes, hipMemcpyDeviceToHost, c->stream));
+        off += align256(o[i].bytes);
+    }
+    const int rc = fp_take_err(c);  // synchronises the copies too
+    if (rc) return rc;
+    off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!o[i].h || !o[i].bytes) continue;
+        memcpy(o[i].h, c->h_stage + off, o[i].bytes);
+        off += align256(o[i].bytes);
+    }
     return FP_OK;
 }
 
@@ -242,21 +285,8 @@ extern "C" int fp_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm_out)
     if (rc) return rc;
     rc = fp_dev_legacy_order_impl(c, &dg, dperm);
     if (rc) return rc;
-    if ((rc = fp_check_err(c))) return rc;
-    if ((rc = copy_back(c, perm_out, dperm, V * 4))) return rc;
-    FP_HIP(hipStreamSynchronize(c->stream));
-    return FP_OK;
-}
-
-static int validate_graph_host(const fp_graph *g) {
-    const uint32_t V = g->n_vertices;
-    if (!g->row_ptr) return FP_EINVAL;
-    if (g->row_ptr[0] != 0 || g->row_ptr[V] != g->n_edges) return FP_ECORRUPT;
-    for (uint32_t v = 0; v < V; ++v)
-        if (g->row_ptr[v + 1] < g->row_ptr[v]) return FP_ECORRUPT;
-    for (uint32_t e = 0; e < g->n_edges; ++e)
-        if (g->col[e] >= V) return FP_ECORRUPT;
-    return FP_OK;
+    const OutCopy o[] = {{perm_out, dperm, V * 4}};
+    return copy_back_all(c, o, 1);
 }
 
 extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, uint32_t *order_out,
@@ -270,10 +300,9 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
         if (n_cycle_out) *n_cycle_out = 0;
         return FP_OK;
     }
-    int rc = validate_graph_host(g);
-    if (rc) return rc;
+    // the CSR is validated on the device (k_check_csr, k_indeg): FP_ECORRUPT
     FP_HIP(hipSetDevice(c->device));
-    rc = fp_stage_reserve(c, (V + 1) * 4 + E * 4 + V + 2 * V * 4 + 8 * 256);
+    int rc = fp_stage_reserve(c, (V + 1) * 4 + E * 4 + V + 2 * V * 4 + 8 * 256);
     if (rc) return rc;
     fp_stage_reset(c);
     fp_graph dg = *g;
@@ -286,12 +315,8 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
     if (rc) return rc;
     rc = fp_dev_levelize_impl(c, &dg, dlev, dord, dcyc);
     if (rc) return rc;
-    if ((rc = fp_check_err(c))) return rc;
-    if ((rc = copy_back(c, level_out, dlev, V * 4))) return rc;
-    if ((rc = copy_back(c, order_out, dord, V * 4))) return rc;
-    if (n_cycle_out && (rc = copy_back(c, n_cycle_out, dcyc, 4))) return rc;
-    FP_HIP(hipStreamSynchronize(c->stream));
-    return FP_OK;
+    const OutCopy o[] = {{level_out, dlev, V * 4}, {order_out, dord, V * 4}, {n_cycle_out, dcyc, 4}};
+    return copy_back_all(c, o, 3);
 }
 
 static int batch_host(fp_ctx *c, const fp_batch *b) {
@@ -324,15 +349,10 @@ static int batch_host(fp_ctx *c, const fp_batch *b) {
     if (rc) return rc;
     rc = fp_dev_place_batch_impl(c, &d);
     if (rc) return rc;
-    if ((rc = fp_check_err(c))) return rc;
-    if ((rc = copy_back(c, b->assign, d.assign, SC * 4))) return rc;
-    if ((rc = copy_back(c, b->reason, d.reason, SC))) return rc;
-    if (b->cost && (rc = copy_back(c, b->cost, d.cost, S * 8))) return rc;
-    if ((rc = copy_back(c, b->cpu_free, d.cpu_free, SN * 4))) return rc;
-    if ((rc = copy_back(c, b->mem_free, d.mem_free, SN * 4))) return rc;
-    if ((rc = copy_back(c, b->conflict_used, d.conflict_used, SN * 4))) return rc;
-    FP_HIP(hipStreamSynchronize(c->stream));
-    return FP_OK;
+    const OutCopy o[] = {{b->assign, d.assign, SC * 4},          {b->reason, d.reason, SC},
+                         {b->cost, d.cost, S * 8},                {b->cpu_free, d.cpu_free, SN * 4},
+                         {b->mem_free, d.mem_free, SN * 4},       {b->conflict_used, d.conflict_used, SN * 4}};
+    return copy_back_all(c, o, 6);
 }
 
 extern "C" int fp_place_batch(fp_ctx *c, const fp_batch *b) {
@@ -396,10 +416,6 @@ extern "C" int fp_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes
     if (rc) return rc;
     rc = fp_dev_feasibility_impl(c, &dc, &dn, dfirst, dcount, dbits);
     if (rc) return rc;
-    if ((rc = fp_check_err(c))) return rc;
-    if ((rc = copy_back(c, first_out, dfirst, C * 4))) return rc;
-    if ((rc = copy_back(c, count_out, dcount, C * 4))) return rc;
-    if (bitmap_out && (rc = copy_back(c, bitmap_out, dbits, WC * N * 8))) return rc;
-    FP_HIP(hipStreamSynchronize(c->stream));
-    return FP_OK;
+    const OutCopy o[] = {{first_out, dfirst, C * 4}, {count_out, dcount, C * 4}, {bitmap_out, dbits, WC * N * 8}};
+    return copy_back_all(c, o, 3);
 }

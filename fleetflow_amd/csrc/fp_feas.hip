@@ -116,7 +116,6 @@ int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *
     if (N && (!ns->cpu_free || !ns->mem_free || !ns->labels || !ns->conflict_used || !ns->schedulable))
         return FP_EINVAL;
     hipStream_t st = c->stream;
-    FP_HIP(hipMemsetAsync(c->d_err, 0, 4, st));
     const uint32_t xb = (C + kBlock * kPer - 1) / (kBlock * kPer);
     // split the node range over blockIdx.y until the grid is >= ~2048 blocks
     uint32_t ysplit = 1;

@@ -18,7 +18,10 @@ struct fp_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    // kernel-side error word (e.g. a CSR index out of range): zeroed per call
+    // kernel-side error word (a CSR index out of range, the pipeline's deadlock guard):
+    // sticky -- kernels atomicMax into it, and only fp_take_err (fp_ctx_sync, the end of
+    // every host-pointer call, the levelizer's mid-call checks) reads and clears it, so an
+    // asynchronous call's error survives later calls until someone reports it
     uint32_t *d_err = nullptr;
     // device workspace: a bump arena reset at the start of every API call
     char *ws = nullptr;
@@ -28,6 +31,10 @@ struct fp_ctx {
     size_t stage_cap = 0, stage_top = 0;
     // pinned host bounce buffer for small read-backs
     uint64_t *h_small = nullptr;
+    // pinned host staging of host-API results: copied to the caller only when every
+    // kernel and every device-to-host copy succeeded (all-or-nothing)
+    char *h_stage = nullptr;
+    size_t h_stage_cap = 0;
     // profiling
     bool profile = false;
     struct Rec { int kid; hipEvent_t a, b; };
@@ -49,8 +56,8 @@ void *fp_stage_take(fp_ctx *c, size_t bytes);
 void fp_prof_begin(fp_ctx *c, int kid, hipEvent_t *a);
 void fp_prof_end(fp_ctx *c, int kid, hipEvent_t a);
 
-// kernel-side error check after a synchronising read-back
-int fp_check_err(fp_ctx *c);
+// synchronise the stream, read the sticky kernel error word and clear it (0 or -FP_E*)
+int fp_take_err(fp_ctx *c);
 
 static inline uint32_t fp_bitwidth(uint64_t v) {
     uint32_t b = 0;

@@ -502,7 +502,6 @@ int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
     if (V == 0) return FP_OK;
     if (!g->has_deps || !perm) return FP_EINVAL;
     hipStream_t st = c->stream;
-    FP_HIP(hipMemsetAsync(c->d_err, 0, 4, st));
     const uint32_t nb = (uint32_t)((V + kSpan - 1) / kSpan);
     int rc = fp_ws_reserve(c, (size_t)(nb + 1) * 8 + 1024);
     if (rc) return rc;
@@ -532,7 +531,6 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     }
     if (!g->has_deps || !g->row_ptr || (E && !g->col) || !level || !order) return FP_EINVAL;
     hipStream_t st = c->stream;
-    FP_HIP(hipMemsetAsync(c->d_err, 0, 4, st));
 
     size_t sort_tmp = 0;
     FP_HIP(rocprim::radix_sort_pairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
@@ -581,18 +579,15 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl,
                                                              pk);
         FP_HIP(hipGetLastError());
-        FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
-        FP_HIP(hipStreamSynchronize(st));
-        if (((uint32_t *)c->h_small)[0]) return -(int)((uint32_t *)c->h_small)[0];
+        // a corrupt CSR (k_check_csr / k_indeg) stops here, before any expansion
+        if ((rc = fp_take_err(c))) return rc;
         if (E) {
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
             k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, g->col, V, state, Q, actl, level, c->d_err, pk);
             FP_HIP(hipGetLastError());
         }
-        FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
         FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &actl[26 * kCtlStride], 4, hipMemcpyDeviceToHost, st));
-        FP_HIP(hipStreamSynchronize(st));
-        if (((uint32_t *)c->h_small)[0]) return -(int)((uint32_t *)c->h_small)[0];
+        if ((rc = fp_take_err(c))) return rc;  // synchronises the read-back above too
         const uint32_t maxl = ((uint32_t *)c->h_small)[2];
         // levels <= max(maxl, 1); the cycle key sorts after every level
         const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
@@ -607,10 +602,8 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     k_lvl_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, V, level, fa, &cnt[0]);
     FP_HIP(hipGetLastError());
     // corrupt CSR => stop before expanding
-    FP_HIP(hipMemcpyAsync(c->h_small, c->d_err, 4, hipMemcpyDeviceToHost, st));
     FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &cnt[0], 4, hipMemcpyDeviceToHost, st));
-    FP_HIP(hipStreamSynchronize(st));
-    if (((uint32_t *)c->h_small)[0]) return -(int)((uint32_t *)c->h_small)[0];
+    if ((rc = fp_take_err(c))) return rc;
     const uint32_t f0 = ((uint32_t *)c->h_small)[2];
     // Levels are enqueued in chunks of kChunk launches with no read-back in between
     // (a level whose frontier is empty is a no-op launch); one read of the last

@@ -59,7 +59,7 @@ constexpr uint32_t CYC = 0x80000000u;
 // Deadlock guard: a wait longer than this (s_memrealtime runs at 100 MHz) aborts the
 // launch with FP_EDEVICE.  Downstream stages legitimately wait for most of a long
 // launch, so the bound is wall-clock time, not an iteration count.
-constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s
+constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s (FLEETPLACE_SPIN_TICKS overrides: tests)
 constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per group)
 #ifndef FP_SPIN_MAX
 #define FP_SPIN_MAX 12              // longest back-off sleep of an idle stage (x 64 cycles)
@@ -84,6 +84,7 @@ struct PipeArgs {
     uint8_t *reason;
     uint64_t *cost;
     uint32_t *err;
+    uint64_t spin_ticks;    // deadlock guard, s_memrealtime ticks (100 MHz)
     uint32_t tc[K], tm[K];  // ascending thresholds, tc[0] = tm[0] = 0
 };
 
@@ -109,7 +110,7 @@ __device__ __forceinline__ void g_st(uint32_t *p, uint32_t v) {
 // Spin on an LDS word until pred holds; bounded, with a workgroup abort flag.
 template <class Pred>
 __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_flag, uint32_t *err,
-                                     uint32_t &iters) {
+                                     uint64_t ticks, uint32_t &iters) {
     uint32_t n = 0;
     uint64_t t0 = 0;
     while (true) {
@@ -120,7 +121,7 @@ __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
             if (!t0) {
                 t0 = now;
-            } else if (now - t0 > SPIN_TICKS) {
+            } else if (now - t0 > ticks) {
                 lds_rel(abort_flag, 1u);
                 if ((threadIdx.x & 63) == 0) atomicMax(err, (uint32_t)(-FP_EDEVICE));
                 return false;
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     if (!t0) {
                         t0 = now;
-                    } else if (now - t0 > SPIN_TICKS) {
+                    } else if (now - t0 > a.spin_ticks) {
                         g_st(a.gabort, 1u);
                         lds_rel(abort_flag, 1u);
                         if (lane == 0) atomicMax(a.err, (uint32_t)(-FP_EDEVICE));
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             k0 += 64;
         } else {
             const uint32_t want = itail;
-            if (!spin(&ictl[0], [want](uint32_t h) { return h != want; }, abort_flag, a.err, st_spin_in)) break;
+            if (!spin(&ictl[0], [want](uint32_t h) { return h != want; }, abort_flag, a.err, a.spin_ticks, st_spin_in)) break;
             const uint32_t slot = itail % R;
             const uint32_t n = ictl[2 + slot];
             if (n & END) break;
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             lds_rel(&octl[0], ohead);
             const uint32_t h = ohead;
             ck_b = STAT_CLK(); ck_fwd += ck_b - ck_a; ck_a = ck_b;
-            if (!spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, st_spin_out)) {
+            if (!spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, a.spin_ticks, st_spin_out)) {
                 alive = false;
                 break;
             }
@@ -608,7 +609,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             ohead++;
             lds_rel(&octl[0], ohead);
             const uint32_t h = ohead;
-            ok = spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, st_spin_out);
+            ok = spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, a.spin_ticks, st_spin_out);
         }
         if (ok) {
             octl[2 + ohead % R] = END;
@@ -881,6 +882,8 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
     a.assign = b->assign; a.reason = b->reason; a.cost = b->cost; a.err = c->d_err;
+    a.spin_ticks = SPIN_TICKS;
+    if (getenv("FLEETPLACE_SPIN_TICKS")) a.spin_ticks = strtoull(getenv("FLEETPLACE_SPIN_TICKS"), nullptr, 10);
     // thresholds: T0 = 0, then K-1 geometric steps from the smallest positive to
     // the largest demand of the batch (any ascending choice is exact; this one
     // only decides how tight the candidate masks are)

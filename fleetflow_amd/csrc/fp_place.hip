@@ -200,6 +200,11 @@ __global__ void k_seg_offsets(uint32_t S, uint32_t C, uint32_t *__restrict__ off
     if (i <= S) off[i] = i * C;
 }
 
+__global__ void k_fill_cost(uint32_t S, uint32_t scen_base, uint64_t *__restrict__ cost) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < S) cost[s] = fpd::pack_cost(0, 0, scen_base + s);
+}
+
 __global__ void k_argmin_cost(const uint64_t *__restrict__ cost, uint32_t n, uint32_t *best) {
     // single block of 1024: min over packed costs; the id field breaks ties
     __shared__ uint64_t red[16];
@@ -236,15 +241,24 @@ static inline unsigned grid_for(size_t n, unsigned block) {
 
 int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     const uint32_t S = b->n_scen, C = b->n_containers, N = b->n_nodes;
-    if (S == 0 || C == 0) return FP_OK;
+    if (S == 0) return FP_OK;
+    // the packed cost keeps 16 bits of the global scenario id (SPEC.md 2.4): more
+    // scenarios would let a wrapped id win a tie it must lose
+    if ((uint64_t)b->scen_base + S > 65536ull) return FP_EOVERFLOW;
+    hipStream_t st = c->stream;
+    if (C == 0) {  // nothing to place: every scenario costs (0 rejected, 0 nodes used)
+        if (b->cost) {
+            k_fill_cost<<<(S + 255) / 256, 256, 0, st>>>(S, b->scen_base, b->cost);
+            FP_HIP(hipGetLastError());
+        }
+        return FP_OK;
+    }
     const size_t SC = (size_t)S * C;
     if (SC > 0xFFFFFFFFull) return FP_EOVERFLOW;  // rocprim segmented sort takes u32 sizes
     if (!b->cpu_m || !b->mem_mib || !b->req_labels || !b->conflict || !b->assign || !b->reason)
         return FP_EINVAL;
     if (N && (!b->cpu_free || !b->mem_free || !b->labels || !b->conflict_used || !b->schedulable))
         return FP_EINVAL;
-    hipStream_t st = c->stream;
-    FP_HIP(hipMemsetAsync(c->d_err, 0, 4, st));
 
     // ---- workspace ----
     // device-wide sorts are sized for the widest key they may take (u64); the

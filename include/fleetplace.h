@@ -20,7 +20,15 @@
  *   - All buffers are caller-owned; no allocation crosses the ABI.
  *   - fp_* take HOST pointers and are synchronous: on error nothing is written.
  *   - fp_dev_* take DEVICE (HBM) pointers of the context's device and are
- *     asynchronous on the context's stream; fp_ctx_sync() reports kernel errors.
+ *     asynchronous on the context's stream.  Kernel-side errors (FP_ECORRUPT input,
+ *     FP_EDEVICE from the placement pipeline's deadlock guard) are sticky: the first
+ *     one raised is kept until fp_ctx_sync() -- or the next host-pointer call, or the
+ *     levelizer's own mid-call check -- reports it and clears it.
+ *     fp_dev_place_batch and fp_dev_levelize read a few words back to size their
+ *     sort keys / level count, so they synchronise the stream once or twice per call;
+ *     their kernels stay queued and asynchronous.
+ *   - fp_ctx_set_stream drains the old stream before switching (the device
+ *     workspace is reused by every call).
  *   - Return 0 (FP_OK) or a negative FP_E* code.  There is no CPU fallback:
  *     fp_ctx_create fails with FP_EDEVICE when no MI355X (gfx950) is present.
  *   - One fp_ctx per host thread; contexts are not shared.
@@ -80,7 +88,9 @@ typedef struct {
 } fp_nodes;
 
 /* S independent what-if scenarios, each C containers on its own N nodes.
- * Every array is scenario-major: container arrays [S][C], node arrays [S][N]. */
+ * Every array is scenario-major: container arrays [S][C], node arrays [S][N].
+ * scen_base + n_scen <= 65536 (the packed cost keeps a 16-bit scenario id), else
+ * FP_EOVERFLOW. */
 typedef struct {
     uint32_t n_scen, scen_base;   /* scen_base: global id of scenario 0 (cost field) */
     uint32_t n_containers, n_nodes;

@@ -1,0 +1,72 @@
+"""Error behaviour of the C ABI (include/fleetplace.h conventions) on the GPU:
+kernel-side errors of asynchronous fp_dev_* calls are sticky until fp_ctx_sync
+(or the next host-pointer call) reports them once and clears them, and the
+host-pointer calls write nothing on error."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pipeline_deadlock_guard_is_reported_by_sync(planner, monkeypatch):
+    """Force the placement pipeline's wall-clock guard (FLEETPLACE_SPIN_TICKS=1: any
+    wait longer than ~2k spin iterations aborts): the launch drains, fp_dev_place_batch
+    itself returns OK (asynchronous), fp_ctx_sync reports FP_EDEVICE exactly once, and a
+    normal run afterwards is clean."""
+    import torch
+    from fleetflow_amd import DevBatch
+    from fleetflow_amd._lib import FP_EDEVICE, FleetplaceError
+    db = DevBatch.allocate(4, 50_000, 5_000, "cuda:0")
+    planner.dev_gen_batch(0x5EED0004, db, 7)
+    snap = db.node_snapshot()
+    monkeypatch.setenv("FLEETPLACE_SPIN_TICKS", "1")
+    planner.dev_place_batch(db)
+    with pytest.raises(FleetplaceError) as e:
+        planner.sync()
+    assert e.value.code == FP_EDEVICE
+    planner.sync()  # reported once, then cleared
+    monkeypatch.delenv("FLEETPLACE_SPIN_TICKS")
+    db.restore_nodes(snap)
+    planner.dev_place_batch(db)
+    planner.sync()
+    assert int((db.reason == 0).sum().item()) > 0
+    del db
+    torch.cuda.empty_cache()
+
+
+def test_dev_levelize_corrupt_csr_reported_once(planner):
+    import torch
+    from fleetflow_amd._lib import FP_ECORRUPT, FleetplaceError
+    dev = "cuda:0"
+    rp = torch.tensor([0, 1, 2], dtype=torch.int32, device=dev)
+    col = torch.tensor([0, 7], dtype=torch.int32, device=dev)  # 7 >= V
+    hd = torch.tensor([0, 1], dtype=torch.uint8, device=dev)
+    lv = torch.empty(2, dtype=torch.int32, device=dev)
+    od = torch.empty(2, dtype=torch.int32, device=dev)
+    nc = torch.empty(1, dtype=torch.int32, device=dev)
+    with pytest.raises(FleetplaceError) as e:
+        planner.dev_levelize(rp, col, hd, lv, od, nc)
+    assert e.value.code == FP_ECORRUPT
+    planner.sync()  # the mid-call check reported and cleared it
+    level, order, ncyc = planner.levelize([0, 1, 1], [1], [0, 1])
+    assert level.tolist() == [0, 1] and order.tolist() == [0, 1] and ncyc == 0
+
+
+def test_host_call_writes_nothing_on_error(planner):
+    from fleetflow_amd._lib import FleetplaceError
+    level = np.full(2, 12345, np.uint32)
+    order = np.full(2, 54321, np.uint32)
+    import ctypes as ct
+    from fleetflow_amd import _lib
+    rp = np.array([0, 1, 2], np.uint32)
+    col = np.array([0, 7], np.uint32)
+    hd = np.array([0, 1], np.uint8)
+    g = _lib.FpGraph(2, 2, rp.ctypes.data, col.ctypes.data, hd.ctypes.data)
+    ncyc = ct.c_uint32(777)
+    rc = _lib.load().fp_levelize(planner._ctx, ct.byref(g), level.ctypes.data_as(_lib.u32p),
+                                 order.ctypes.data_as(_lib.u32p), ct.byref(ncyc))
+    assert rc == _lib.FP_ECORRUPT
+    assert level.tolist() == [12345, 12345] and order.tolist() == [54321, 54321] and ncyc.value == 777
+    with pytest.raises(FleetplaceError):
+        planner.levelize([0, 2, 1], [1, 0], [0, 1])  # row_ptr not monotone
+    planner.sync()

@@ -307,6 +307,65 @@ def test_config4_scenarios_full_size(planner, O):
     assert int(best.item()) == int(np.argmin(costs))
 
 
+def test_place_batch_no_containers(planner):
+    """C == 0 with S > 0: nothing placed, and every scenario's cost is still written
+    (0 rejected, 0 nodes used, its own id; SPEC.md 2.4)."""
+    S, N, base = 3, 40, 9
+    nodes = [np.full(S * N, 100, np.uint32), np.full(S * N, 100, np.uint32), np.zeros(S * N, np.uint32),
+             np.zeros(S * N, np.uint32), np.ones(S * N, np.uint8)]
+    empty = np.zeros(0, np.uint32)
+    assign, reason, cost, after = planner.place_batch(S, 0, N, [empty] * 4, nodes, scen_base=base)
+    assert assign.size == 0 and reason.size == 0
+    assert [int(c) for c in cost] == [base + s for s in range(S)]
+    assert np.array_equal(after[0], nodes[0])
+
+
+def test_place_batch_scenario_id_limit(planner):
+    """scen_base + S > 65536 would wrap the packed cost's 16-bit id: refused."""
+    from fleetflow_amd._lib import FP_EOVERFLOW, FleetplaceError
+    one = [np.ones(2, np.uint32)] * 4
+    nodes = [np.full(2, 9, np.uint32), np.full(2, 9, np.uint32), np.zeros(2, np.uint32), np.zeros(2, np.uint32),
+             np.ones(2, np.uint8)]
+    planner.place_batch(2, 1, 1, one, nodes, scen_base=65534)
+    with pytest.raises(FleetplaceError) as e:
+        planner.place_batch(2, 1, 1, one, nodes, scen_base=65535)
+    assert e.value.code == FP_EOVERFLOW
+
+
+def test_config4_bench_size_batch(planner, O):
+    """The bench geometry at scale: 256 scenarios of 50k x 5k in one dev_place_batch
+    (two segments of four 10-group stages, many tickets in flight).  Scenarios
+    {0, mid, last} are checked plan-for-plan against the oracle, and the argmin
+    against the oracle's costs of all 256 scenarios."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from fleetflow_amd import DevBatch
+    S, C, N, base, seed = 256, 50_000, 5_000, 1024, SEED + 4
+    db = DevBatch.allocate(S, C, N, "cuda:0", scen_base=base)
+    planner.dev_gen_batch(seed, db, 7)
+    planner.dev_place_batch(db)
+    planner.sync()
+    costs = db.cost.cpu().numpy().view(np.uint64)
+
+    def oracle_cost(s):
+        cont, nodes = O.gen_scenario(seed, base + s, C, N, 7)
+        ea, er, _, _ = O.place(cont, nodes)
+        return s, ea, er, O.cost(ea, N, base + s)
+
+    with ThreadPoolExecutor(16) as ex:
+        res = list(ex.map(oracle_cost, range(S)))
+    for s, ea, er, ec in res:
+        assert int(costs[s]) == ec, s
+        if s in (0, S // 2, S - 1):
+            assert np.array_equal(db.assign[s * C:(s + 1) * C].cpu().numpy().view(np.uint32), ea), s
+            assert np.array_equal(db.reason[s * C:(s + 1) * C].cpu().numpy(), er), s
+    best = torch.empty(1, dtype=torch.int32, device="cuda:0")
+    planner.dev_argmin_cost(db.cost, best)
+    assert int(best.item()) == int(np.argmin([r[3] for r in res]))
+    del db
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("case", ["all_equal", "cpu_const", "mem_const", "rank_limit", "past_rank_limit",
                                   "dense_wide", "zero_mix"])
 def test_ffd_sort_key_compression(case, planner, O):
@@ -397,7 +456,8 @@ def test_ffd_segments_batch_and_cycles(planner, O):
 
 def test_config3_full_size(planner, O):
     """BASELINE config 3: 1M containers x 100k nodes with label anti-affinity, one
-    scenario (20 segments), bit-exact against the oracle at full size."""
+    scenario (the narrow geometry: 391 segments of four one-group stages), bit-exact
+    against the oracle at full size."""
     cont, nodes = O.gen_scenario(SEED + 3, 0, 1_000_000, 100_000, 7)
     assign, reason = _check_ffd(planner, O, cont, nodes)
     assert (reason == 1).any() and (reason == 0).any()

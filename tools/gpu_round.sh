@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU session: error-path tests (isolated, short limit), the -m gpu suite, the bench
+# (config 4 at 4096 + config 3 leg + CPU baseline), then the rocprofv3 passes.
+# Usage: tools/gpu_round.sh <tag> [steps...]   steps: errors tests bench prof (default: all)
+set -o pipefail
+tag=${1:?tag}; shift
+steps=${*:-errors tests bench prof}
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$root" || exit 1
+mkdir -p gpurun_out
+log=gpurun_out/${tag}
+for s in $steps; do
+  case $s in
+    errors)
+      timeout -k 10 150 python -u -m pytest tests/test_gpu_errors.py -x -v --timeout 120 --timeout-method thread \
+        > ${log}_errors.log 2>&1 || { echo "errors step failed"; tail -30 ${log}_errors.log; exit 1; } ;;
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > ${log}_tests.log 2>&1 || { echo "tests step failed"; tail -40 ${log}_tests.log; exit 1; }
+      tail -3 ${log}_tests.log ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > ${log}_bench.json 2> ${log}_bench.err \
+        || { echo "bench failed"; tail -30 ${log}_bench.err; exit 1; }
+      cat ${log}_bench.json ;;
+    prof)
+      timeout -k 10 1000 bash tools/profile.sh $tag || { echo "profile failed"; exit 1; } ;;
+    stats)
+      timeout -k 10 300 python -u tools/pipe_stats.py 512 > ${log}_pipe_stats.txt 2>&1 || { echo "stats failed"; tail ${log}_pipe_stats.txt; exit 1; }
+      cat ${log}_pipe_stats.txt ;;
+  esac
+done
+echo "gpu_round $tag done: $steps"
