@@ -69,7 +69,8 @@ uint32_t fpo_levelize(uint32_t V, const uint32_t *row_ptr, const uint32_t *col,
 /* ------------------------------------------------------------------------- */
 /* A6  SPEC.md 2.3: FFD key (cpu desc, mem desc, index asc).                  */
 /* ------------------------------------------------------------------------- */
-static const uint32_t *g_cpu, *g_mem;
+/* thread-local: the bench CPU baseline and tests run the oracle on many host threads */
+static _Thread_local const uint32_t *g_cpu, *g_mem;
 static int ffd_cmp(const void *a, const void *b) {
     uint32_t i = *(const uint32_t *)a, j = *(const uint32_t *)b;
     if (g_cpu[i] != g_cpu[j]) return g_cpu[i] > g_cpu[j] ? -1 : 1;

@@ -157,3 +157,20 @@ def test_ffd_order_key(O, P):
 def test_cost_packing(O, P):
     a = [0, 0, 3, NONE, 3, 7]
     assert O.cost(a, 8, 5) == P.cost(a, 5) == (1 << 40) | (3 << 16) | 5
+
+
+def test_oracle_is_thread_safe(O):
+    """The bench CPU baseline and the bench-size GPU test run the oracle on many host
+    threads at once: concurrent plans must equal sequential ones (the FFD sort's
+    comparator state is thread-local)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def plan(s):
+        cont, nodes = O.gen_scenario(0x5EED0004, s, 4000, 400, 7)
+        a, r, _, _ = O.place(cont, nodes)
+        return a.tobytes() + r.tobytes()
+
+    seq = [plan(s) for s in range(24)]
+    with ThreadPoolExecutor(8) as ex:
+        for _ in range(3):
+            assert list(ex.map(plan, range(24))) == seq
