@@ -23,10 +23,11 @@
 // clearing bits on placement and a stale mask is always a superset: only
 // candidate groups get the exact check.
 #include "fp_internal.h"
-// Stages of 2..10 groups (the wide geometry: config 4 and other many-scenario batches) run
-// the hand-scheduled candidate loop of fp_pipe_asm.h, one-group stages (configs 2, 3, 5) a
-// specialised C++ loop; -DFP_NO_ASM builds the C++ loops everywhere (A/B, reference)
-#ifndef FP_NO_ASM
+// The candidate loop is group-major (below): every register access uses a compile-time
+// group index.  -DFP_LEGACY_LOOP builds round 1's container-major loops instead (the
+// hand-scheduled fp_pipe_asm.h loop for 2..10-group stages, C++ elsewhere; add
+// -DFP_NO_ASM for C++ everywhere) -- kept for A/B measurements.
+#if defined(FP_LEGACY_LOOP) && !defined(FP_NO_ASM)
 #define FP_ASM
 #endif
 #include "fp_pipe_asm.h"
@@ -173,8 +174,8 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 //   CTL : (W-1)*8 u32 + 8 u32   per link [0]=head [1]=tail [2..2+R)=slot counts; then
 //                               CNT [0]=n_used [1]=n_rej [2]=abort
 //   D   : (W-1)*R*NF*64 u32     ring slots, field-major
-// a tile's records of one kind, one register per group (a plain array: register-
-// promoted, read and written through s_set_gpr_idx; a pinned tuple in the asm build)
+// a tile's records of one kind, one register per group (a plain array, register-promoted
+// with static indices; a pinned tuple in the legacy asm build)
 #ifdef FP_ASM
 template <uint32_t G>
 using RecT = typename std::conditional<(G >= 2 && G <= 10), rec10, uint32_t[G]>::type;
@@ -394,7 +395,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         const unsigned long long tl_pre = ck_b;
         const uint32_t tl_checks0 = st_checks, tl_hits0 = st_hits, tl_todo = (uint32_t)__popcll(todo);
 #endif
-#ifdef FP_ASM
+#ifdef FP_LEGACY_LOOP
+#  ifdef FP_ASM
         // Exact first fit, container by container in FFD order: the hand-scheduled
         // loop (fp_pipe_asm.h) for 2..10-group stages.  Same algorithm as the C++ loop below.
         if constexpr (G >= 2 && G <= 10) {
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                           lane_sel, maddr, (gbase * 64u), nchk, nhit);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
         } else
-#endif
+#  endif
         if constexpr (G == 1) {
             // one-group stages (few scenarios): every todo container has exactly one
             // candidate group, so one check each and no candidate bookkeeping
@@ -501,6 +503,79 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                 }
             }
         }
+#else
+        // Exact first fit, GROUP-major.  Container t's checks must see every earlier
+        // container's placement in the group being checked, and nothing else matters to
+        // it: placements in other groups touch other nodes.  So instead of walking the
+        // containers in order, each checking its candidate groups, the groups are walked
+        // in order (a compile-time loop) and each group takes the containers that reach
+        // it in container order: group g's queue is every todo lane whose next candidate
+        // group is g.  A container that finds no feasible node in g moves on to its next
+        // candidate group, which is > g and so still to come.  Every container sees group
+        // g after exactly the earlier containers that reached g -- the sequential first
+        // fit, bit for bit -- and every record access has a static register index (no
+        // s_set_gpr_idx windows, no indexed copies).
+        {
+            uint32_t nxt = ((todo >> lane) & 1ull) ? (uint32_t)__builtin_ctz(cand | (1u << G)) : G;
+#ifndef FP_NO_ASM
+            // the hand-scheduled loop of fp_pipe_asm.h, one asm block per (static) group
+            const uint32_t lane_sel = lane < 32u ? 0xFFFFFFFFu : 0u;
+            const uint32_t maddr0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint64_t *)(
+                Mw + (lane & (K - 1)) * 2 + (lane >> 5));
+            uint32_t nchk = 0, nhit = 0;
+#pragma unroll
+            for (uint32_t g = 0; g < G; ++g) {
+                const uint64_t q = __builtin_amdgcn_ballot_w64(nxt == g);
+                if (q)
+                    fpp_asm_group(q, placed, my_assign, usedbits, nxt, rcf[g], rmf[g], rcu[g], rlab[g], cpu, mem, req,
+                                  conf, cand, my_t, lane_sel, maddr0 + g * (K * 2 * 8), (gbase + g) * 64u, 1u << g,
+                                  ~((2u << g) - 1u), G, nchk, nhit);
+            }
+            if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
+#else
+#pragma unroll
+            for (uint32_t g = 0; g < G; ++g) {
+                uint64_t q = __builtin_amdgcn_ballot_w64(nxt == g);
+                while (q) {
+                    const uint32_t ti = (uint32_t)__builtin_ctzll(q);
+                    q &= q - 1;
+                    const uint32_t c_cpu = __builtin_amdgcn_readlane(cpu, ti);
+                    const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
+                    const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
+                    const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
+                    const uint32_t x = rcf[g], y = rmf[g], z = rcu[g];
+                    if (STAT_ON) st_checks++;
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
+                                       __builtin_amdgcn_ballot_w64(((rlab[g] & c_req) | (z & c_conf)) == 0u);
+                    if (m) {
+                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                        const uint32_t oc = __builtin_amdgcn_readlane(x, l);
+                        const uint32_t om = __builtin_amdgcn_readlane(y, l);
+                        const uint32_t nc = oc - c_cpu, nm = om - c_mem;
+                        const bool me = lane == l;
+                        rcf[g] = me ? nc : x;
+                        rmf[g] = me ? nm : y;
+                        rcu[g] = me ? (z | c_conf) : z;
+                        usedbits |= me ? (1u << g) : 0u;
+                        // bucket masks: lanes 0-31 hold the cpu thresholds, 32-63 the mem ones;
+                        // clear bit l where the placement crossed the threshold
+                        const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
+                        const bool crossed = (my_t <= ov) & (my_t > nv);
+                        atomicAnd((unsigned long long *)&Mw[(size_t)g * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
+                                  crossed ? ~(1ull << l) : ~0ull);
+                        placed |= 1ull << ti;
+                        my_assign = (uint32_t)fp_writelane((int)((gbase + g) * 64 + l), (int)ti, (int)my_assign);
+                        if (STAT_ON) st_hits++;
+                    } else {
+                        // later candidate groups of container ti (none: it leaves the tile)
+                        const uint32_t cc = (uint32_t)__builtin_amdgcn_readlane(cand, ti) & ~((2u << g) - 1u);
+                        nxt = (uint32_t)fp_writelane((int)(cc ? (uint32_t)__builtin_ctz(cc) : G), (int)ti, (int)nxt);
+                    }
+                }
+            }
+#endif
+        }
+#endif
         if (zs_g < G) {
             // all-zero containers change no record: each takes the first schedulable node
             const uint64_t zm = __builtin_amdgcn_ballot_w64(zero);
@@ -520,7 +595,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             a.reason[cb + idx] = FP_REASON_OK;
         }
 #ifdef FP_PIPE_STATS
-        if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B) {
+        if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B && b * W + w < 16) {
             // global stage b * W + w; per batch: ready, prescan end, loop end, checks, hits, todo
             unsigned long long *tl = &g_pipe_tl[((size_t)(b * W + w) * TL_B + tl_idx) * 8];
             tl[0] = ck_t0_batch; tl[1] = tl_pre; tl[2] = tl_cand;

@@ -137,4 +137,108 @@ __device__ __forceinline__ void fpp_asm_batch(uint64_t &todo, uint64_t &placed, 
           "v86", "v87");
 }
 
+// Group-major candidate loop for ONE group g (the default build): exact first fit of the
+// containers queued on group g, in lane (= FFD) order.  Same checks and updates as
+// fpp_asm_batch, but the group's four records are plain "+v" operands -- the group index
+// is a compile-time constant of the caller, so there is no s_set_gpr_idx window and no
+// indexed copy: a check is 4 readlanes, 3 compares, 2 SALU ANDs and a branch.  A miss
+// moves the container to its next candidate group (nxt lane ti = first cand bit above g,
+// or G for none); a hit updates lane l of the records with v_writelane, clears the bucket
+// mask bits the placement crossed (one ds_mskor_b64) and records the assignment.
+//   q       lanes queued on g (consumed)       gb64   (gbase + g) * 64
+//   gbit    1 << g  (used-node bit)            nmask  ~((2 << g) - 1): candidate groups above g
+//   gnone   G (no further candidate)           maddr  LDS address of this lane's mask word of g
+__device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint32_t &asg, uint32_t &used,
+                                              uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
+                                              uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
+                                              uint32_t cand, uint32_t my_t, uint32_t lsel, uint32_t maddr,
+                                              uint32_t gb64, uint32_t gbit, uint32_t nmask, uint32_t gnone,
+                                              uint32_t &nchk, uint32_t &nhit) {
+    uint32_t ti, ccpu, cmem, creq, cconf, l, oc, om, ocu, ous, m0sv, t0, t1;
+    uint64_t tbit, m, m2;
+    asm volatile(
+        "s_mov_b32 %[m0sv], m0\n\t"
+        "v_mov_b32 v82, 1\n\t"
+        "v_mov_b32 v83, 0\n\t"
+        "v_mov_b32 v84, 0\n\t"
+        "v_mov_b32 v85, 0\n\t"
+        "s_cmp_eq_u64 %[q], 0\n\t"
+        "s_cbranch_scc1 .Lfpg_end%=\n"
+        ".Lfpg_cont%=:\n\t"
+        "s_ff1_i32_b64 %[ti], %[q]\n\t"
+        "s_lshl_b64 %[tbit], 1, %[ti]\n\t"
+        "s_andn2_b64 %[q], %[q], %[tbit]\n\t"
+        "v_readlane_b32 %[ccpu], %[cpu], %[ti]\n\t"
+        "v_readlane_b32 %[cmem], %[mem], %[ti]\n\t"
+        "v_readlane_b32 %[creq], %[req], %[ti]\n\t"
+        "v_readlane_b32 %[cconf], %[conf], %[ti]\n\t"
+        FPP_ASM_CNT_CHECK
+        "v_cmp_ge_u32_e64 %[m], %[rcf], %[ccpu]\n\t"
+        "v_cmp_ge_u32_e64 %[m2], %[rmf], %[cmem]\n\t"
+        "v_and_b32_e32 %[t0], %[creq], %[rlab]\n\t"
+        "v_and_or_b32 %[t0], %[rcu], %[cconf], %[t0]\n\t"
+        "s_and_b64 %[m], %[m], %[m2]\n\t"
+        "v_cmp_eq_u32_e64 %[m2], 0, %[t0]\n\t"
+        "s_and_b64 %[m], %[m], %[m2]\n\t"
+        "s_cbranch_scc1 .Lfpg_hit%=\n\t"
+        // miss: the container's next candidate group (none: gnone)
+        "v_readlane_b32 %[oc], %[cand], %[ti]\n\t"
+        "s_and_b32 %[oc], %[oc], %[nmask]\n\t"
+        "s_ff1_i32_b32 %[om], %[oc]\n\t"
+        "s_cmp_eq_u32 %[oc], 0\n\t"
+        "s_cselect_b32 %[om], %[gnone], %[om]\n\t"
+        "s_mov_b32 m0, %[ti]\n\t"
+        "v_writelane_b32 %[nxt], %[om], m0\n\t"
+        "s_cmp_lg_u64 %[q], 0\n\t"
+        "s_cbranch_scc1 .Lfpg_cont%=\n\t"
+        "s_branch .Lfpg_end%=\n"
+        ".Lfpg_hit%=:\n\t"
+        FPP_ASM_CNT_HIT
+        "s_ff1_i32_b64 %[l], %[m]\n\t"
+        "v_readlane_b32 %[oc], %[rcf], %[l]\n\t"
+        "v_readlane_b32 %[om], %[rmf], %[l]\n\t"
+        "v_readlane_b32 %[ocu], %[rcu], %[l]\n\t"
+        "v_readlane_b32 %[ous], %[used], %[l]\n\t"
+        "s_mov_b32 m0, %[l]\n\t"
+        "s_sub_u32 %[ccpu], %[oc], %[ccpu]\n\t"    // new cpu_free
+        "s_sub_u32 %[cmem], %[om], %[cmem]\n\t"    // new mem_free
+        "s_or_b32 %[ocu], %[ocu], %[cconf]\n\t"    // new conflict_used
+        "s_or_b32 %[ous], %[ous], %[gbit]\n\t"     // node used
+        "v_writelane_b32 %[rcf], %[ccpu], m0\n\t"
+        "v_writelane_b32 %[rmf], %[cmem], m0\n\t"
+        "v_writelane_b32 %[rcu], %[ocu], m0\n\t"
+        "v_writelane_b32 %[used], %[ous], m0\n\t"
+        // bucket masks (lanes 0-31 cpu, 32-63 mem): clear bit l where T <= old && T > new
+        "v_mov_b32 %[t0], %[om]\n\t"
+        "v_bfi_b32 %[t0], %[lsel], %[oc], %[t0]\n\t"
+        "v_mov_b32 %[t1], %[cmem]\n\t"
+        "v_bfi_b32 %[t1], %[lsel], %[ccpu], %[t1]\n\t"
+        "v_cmp_le_u32_e64 %[m], %[myt], %[t0]\n\t"
+        "v_cmp_gt_u32_e64 %[m2], %[myt], %[t1]\n\t"
+        "s_and_b64 %[m], %[m], %[m2]\n\t"
+        "v_lshlrev_b64 v[80:81], %[l], v[82:83]\n\t"
+        "v_cndmask_b32_e64 v80, 0, v80, %[m]\n\t"
+        "v_cndmask_b32_e64 v81, 0, v81, %[m]\n\t"
+        "ds_mskor_b64 %[maddr], v[80:81], v[84:85]\n\t"
+        // assignment of lane ti: (gbase + g) * 64 + l
+        "s_or_b32 %[oc], %[gb64], %[l]\n\t"
+        "s_mov_b32 m0, %[ti]\n\t"
+        "v_writelane_b32 %[asg], %[oc], m0\n\t"
+        "s_or_b64 %[placed], %[placed], %[tbit]\n\t"
+        "s_cmp_lg_u64 %[q], 0\n\t"
+        "s_cbranch_scc1 .Lfpg_cont%=\n"
+        ".Lfpg_end%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b32 m0, %[m0sv]"
+        : [q] "+s"(q), [placed] "+s"(placed), [asg] "+v"(asg), [used] "+v"(used), [nxt] "+v"(nxt),
+          [rcf] "+v"(rcf), [rmf] "+v"(rmf), [rcu] "+v"(rcu), [nchk] "+s"(nchk), [nhit] "+s"(nhit),
+          [ti] "=&s"(ti), [ccpu] "=&s"(ccpu), [cmem] "=&s"(cmem), [creq] "=&s"(creq), [cconf] "=&s"(cconf),
+          [l] "=&s"(l), [oc] "=&s"(oc), [om] "=&s"(om), [ocu] "=&s"(ocu), [ous] "=&s"(ous), [m0sv] "=&s"(m0sv),
+          [tbit] "=&s"(tbit), [m] "=&s"(m), [m2] "=&s"(m2), [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [cand] "v"(cand),
+          [myt] "v"(my_t), [lsel] "v"(lsel), [maddr] "v"(maddr), [gb64] "s"(gb64), [gbit] "s"(gbit),
+          [nmask] "s"(nmask), [gnone] "s"(gnone)
+        : "scc", "memory", "v80", "v81", "v82", "v83", "v84", "v85");
+}
+
 }  // namespace fpp
