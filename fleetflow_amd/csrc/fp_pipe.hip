@@ -33,6 +33,7 @@
 #include "fp_pipe_asm.h"
 #include <stdlib.h>
 #include <type_traits>
+#include <utility>
 
 #ifdef FP_PIPE_STATS
 // diagnostics build only: per stage w: [0] visits [1] cand checks [2] hits [3] batches
@@ -184,13 +185,34 @@ template <uint32_t G>
 using RecT = uint32_t[G];
 #endif
 
-template <uint32_t G>
-__global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
+// the group-major loop over a stage's groups, g a compile-time constant in every call
+template <uint32_t G, uint32_t... gs, class Rec>
+__device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
+                                           uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
+                                           Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
+                                           uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lsel,
+                                           uint32_t maddr0, uint32_t gb64, uint32_t &nchk, uint32_t &nhit) {
+    (
+        [&] {
+            const uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
+            if (q)
+                fpp_asm_group<gs, G>(q, placed, asg, gs < 32 ? used : used_hi, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs],
+                                     cpu, mem, req, conf, cand, cand_hi, my_t, lsel, maddr0, gb64, nchk, nhit);
+        }(),
+        ...);
+}
+
+// BLK: 1024 for multi-stage segments (W <= 16 waves, <= 128 VGPRs each); 64 for the
+// one-wave segments of the wide geometry, whose 13..40 groups of records need up to 256 VGPRs
+template <uint32_t G, uint32_t BLK>
+__global__ __launch_bounds__(BLK) void k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = a.W, R = a.R, B = a.B;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t C = a.C, N = a.N;
+    // per-lane group bit sets (schedulable / candidate groups): 64-bit above 32 groups
+    using GM = typename std::conditional<(G > 32), uint64_t, uint32_t>::type;
 
     uint64_t *M = reinterpret_cast<uint64_t *>(smem);
     uint32_t *CTL = reinterpret_cast<uint32_t *>(M + (size_t)W * G * K * 2);
@@ -221,7 +243,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
     // would pass, never reaches the check (placed on the tile's first schedulable node).
     // rlab holds ~labels: label and conflict tests become one ((~lab & req) | (cu & conf)) == 0.
     RecT<G> rcf, rmf, rcu, rlab;
-    uint32_t schedbits = 0, usedbits = 0;               // bit g for node (g, lane)
+    GM schedbits = 0;                                   // bit g: node (g, lane) schedulable
+    uint32_t usedbits = 0, used_hi = 0;                 // bit g (g - 32 in used_hi): node (g, lane) used
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t n = (gbase + g) * 64 + lane;
@@ -231,12 +254,12 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         rmf[g] = sc ? a.mf[nb + n] : 0u;
         rcu[g] = sc ? a.cu[nb + n] : 0xFFFFFFFFu;
         rlab[g] = sc ? ~a.lab[nb + n] : 0xFFFFFFFFu;
-        schedbits |= sc ? (1u << g) : 0u;
+        schedbits |= sc ? (GM(1) << g) : GM(0);
     }
     uint32_t zs_g = G, zs_l = 0;  // the tile's first schedulable node (all-zero containers)
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
-        const uint64_t sm = __builtin_amdgcn_ballot_w64(((schedbits >> g) & 1u) != 0u);
+        const uint64_t sm = __builtin_amdgcn_ballot_w64(((schedbits >> g) & 1u) != 0);
         if (zs_g == G && sm) {
             zs_g = g;
             zs_l = (uint32_t)__builtin_ctzll(sm);
@@ -374,14 +397,14 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         const uint32_t qc = wave_min(valid ? cpu : 0xFFFFFFFFu), qm = wave_min(valid ? mem : 0xFFFFFFFFu);
         // every mask load is issued before the first use (no per-group LDS round trip)
         const uint32_t oc = kc * 2, om = km * 2 + 1;
-        uint32_t cand = 0;
+        GM cand = 0;
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
             const uint64_t e = __builtin_amdgcn_ballot_w64((rcf[g] >= qc) & (rmf[g] >= qm));
             const uint64_t *mg = Mw + (size_t)g * K * 2;
-            cand |= (mg[oc] & mg[om] & e) ? 1u << g : 0u;
+            cand |= (mg[oc] & mg[om] & e) ? GM(1) << g : GM(0);
         }
-        cand = valid ? cand : 0u;
+        cand = valid ? cand : GM(0);
         const bool zero = valid && (cpu | mem | req | conf) == 0u;
         uint64_t todo = __builtin_amdgcn_ballot_w64(cand != 0 && !zero);
         uint64_t placed = 0;
@@ -516,21 +539,16 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         // fit, bit for bit -- and every record access has a static register index (no
         // s_set_gpr_idx windows, no indexed copies).
         {
-            uint32_t nxt = ((todo >> lane) & 1ull) ? (uint32_t)__builtin_ctz(cand | (1u << G)) : G;
+            uint32_t nxt = ((todo >> lane) & 1ull) ? (cand ? (uint32_t)__builtin_ctzll((uint64_t)cand) : G) : G;
 #ifndef FP_NO_ASM
             // the hand-scheduled loop of fp_pipe_asm.h, one asm block per (static) group
             const uint32_t lane_sel = lane < 32u ? 0xFFFFFFFFu : 0u;
             const uint32_t maddr0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint64_t *)(
                 Mw + (lane & (K - 1)) * 2 + (lane >> 5));
             uint32_t nchk = 0, nhit = 0;
-#pragma unroll
-            for (uint32_t g = 0; g < G; ++g) {
-                const uint64_t q = __builtin_amdgcn_ballot_w64(nxt == g);
-                if (q)
-                    fpp_asm_group(q, placed, my_assign, usedbits, nxt, rcf[g], rmf[g], rcu[g], rlab[g], cpu, mem, req,
-                                  conf, cand, my_t, lane_sel, maddr0 + g * (K * 2 * 8), (gbase + g) * 64u, 1u << g,
-                                  ~((2u << g) - 1u), G, nchk, nhit);
-            }
+            fpp_groups<G>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits, used_hi, rcf, rmf,
+                          rcu, rlab, cpu, mem, req, conf, (uint32_t)cand, (uint32_t)((uint64_t)cand >> 32), my_t,
+                          lane_sel, maddr0, __builtin_amdgcn_readfirstlane(gbase * 64u), nchk, nhit);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
 #else
 #pragma unroll
@@ -556,7 +574,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                         rcf[g] = me ? nc : x;
                         rmf[g] = me ? nm : y;
                         rcu[g] = me ? (z | c_conf) : z;
-                        usedbits |= me ? (1u << g) : 0u;
+                        if (g < 32) usedbits |= me ? (1u << g) : 0u;
+                        else used_hi |= me ? (1u << (g & 31)) : 0u;
                         // bucket masks: lanes 0-31 hold the cpu thresholds, 32-63 the mem ones;
                         // clear bit l where the placement crossed the threshold
                         const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
@@ -568,8 +587,10 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
                         if (STAT_ON) st_hits++;
                     } else {
                         // later candidate groups of container ti (none: it leaves the tile)
-                        const uint32_t cc = (uint32_t)__builtin_amdgcn_readlane(cand, ti) & ~((2u << g) - 1u);
-                        nxt = (uint32_t)fp_writelane((int)(cc ? (uint32_t)__builtin_ctz(cc) : G), (int)ti, (int)nxt);
+                        const uint64_t cl = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cand, ti);
+                        const uint64_t ch = (uint32_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)cand >> 32), ti);
+                        const uint64_t cc = ((ch << 32) | cl) & ~((2ull << g) - 1ull);
+                        nxt = (uint32_t)fp_writelane((int)(cc ? (uint32_t)__builtin_ctzll(cc) : G), (int)ti, (int)nxt);
                     }
                 }
             }
@@ -582,7 +603,8 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
             if (zm) {
                 placed |= zm;
                 my_assign = zero ? (gbase + zs_g) * 64 + zs_l : my_assign;
-                usedbits |= lane == zs_l ? (1u << zs_g) : 0u;
+                if (zs_g < 32) usedbits |= lane == zs_l ? (1u << zs_g) : 0u;
+                else used_hi |= lane == zs_l ? (1u << (zs_g & 31)) : 0u;
             }
         }
         ck_b = STAT_CLK(); ck_cand += ck_b - ck_a; ck_a = ck_b;
@@ -693,7 +715,7 @@ __global__ __launch_bounds__(1024) void k_ffd_pipe(const PipeArgs a) {
         }
     }
     {  // nodes of this stage that received a container
-        uint32_t u = (uint32_t)__popc(usedbits);
+        uint32_t u = (uint32_t)__popc(usedbits) + (uint32_t)__popc(used_hi);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) u += (uint32_t)__shfl_xor((int)u, o);
         n_used = u;
@@ -815,10 +837,12 @@ size_t lds_bytes(uint32_t W, uint32_t G, uint32_t R) {
 }
 
 // G is a template parameter (records are register arrays); one instantiation per G
-template <uint32_t G>
+template <uint32_t G, uint32_t BLK = 1024>
 static int launch_g(hipStream_t st, unsigned grid, unsigned block, size_t lds, const PipeArgs &a) {
-    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe<G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_ffd_pipe<G><<<grid, block, lds, st>>>(a);
+    if (block > BLK) return FP_EINVAL;
+    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe<G, BLK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    k_ffd_pipe<G, BLK><<<grid, block, lds, st>>>(a);
     return FP_OK;
 }
 
@@ -827,6 +851,18 @@ static const launch_fn kLaunch[MAX_G + 1] = {
     nullptr,         launch_g<1>,  launch_g<2>,  launch_g<3>,  launch_g<4>,  launch_g<5>,
     launch_g<6>,     launch_g<7>,  launch_g<8>,  launch_g<9>,  launch_g<10>, launch_g<11>,
     launch_g<12>,    launch_g<13>, launch_g<14>, launch_g<15>, launch_g<16>};
+// one-wave segments (W = 1) of 13..40 groups: G rounded up to a multiple of 4 (the padding
+// groups hold unschedulable records, which no container fits)
+constexpr uint32_t MAX_G_WIDE = 40;
+#ifndef FP_LEGACY_LOOP
+static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {
+    nullptr, nullptr, nullptr, nullptr, launch_g<16, 64>, launch_g<20, 64>,
+    launch_g<24, 64>, launch_g<28, 64>, launch_g<32, 64>, launch_g<36, 64>, launch_g<40, 64>};
+static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G > 12; }
+#else  // round 1's loops take at most 16 groups per stage
+static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {nullptr};
+static inline bool wide_g(uint32_t, uint32_t) { return false; }
+#endif
 
 }  // namespace fpp
 
@@ -871,20 +907,30 @@ bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint
     const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
     // FLEETPLACE_PIPE_SEG: groups per segment (tuning experiments and tests)
     const int forced_seg = getenv("FLEETPLACE_PIPE_SEG") ? atoi(getenv("FLEETPLACE_PIPE_SEG")) : 0;
-    // Few scenarios leave the GPU idle: one group (64 nodes) per stage then shortens
-    // each check (no register indexing) -- config 2 (1 x 10k x 1k): 2.39 ms vs 3.02 ms
-    // with 10-group stages; config 3 (1 x 1M x 100k): 160 ms vs 181 ms.  Many scenarios keep 10-group
-    // stages: stages of 1-5 groups put more waves on a CU than it can issue.
+    // Few scenarios leave the GPU idle: one group (64 nodes) per stage then shortens the
+    // chain -- config 2 (1 x 10k x 1k): 2.39 ms vs 3.02 ms with 10-group stages; config 3
+    // (1 x 1M x 100k): 160 ms vs 181 ms.  Many scenarios get one-wave segments of up to 40
+    // groups (W = 1): the stages of a segment were busy one at a time anyway (the
+    // placement frontier moves through them), so one wave does the same work in about the
+    // same time while a scenario needs fewer registers than with 4-stage segments.
     const bool narrow = (uint64_t)S * NG <= kNarrowWaves;
+    // one-wave segments hold at most 32 groups: 28 groups take 233 VGPRs (two waves per
+    // SIMD), 36-40 groups spill
     const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg
-                                : narrow ? 4u : MAX_SEG_GROUPS;
+                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : 32u;
     const uint32_t B = (NG + seg_groups - 1) / seg_groups;
     const uint32_t per_seg = (NG + B - 1) / B;
+    const uint32_t first_w = forced_w > 0 ? (uint32_t)forced_w : narrow ? 4u : 1u;
     // a forced stage count is tried first; sizes it cannot serve fall back to the list
-    for (uint32_t W : {forced_w > 0 ? (uint32_t)forced_w : 4u, 4u, 8u, 2u, 1u, 12u, 16u}) {
+    for (uint32_t W : {first_w, 4u, 8u, 2u, 1u, 12u, 16u}) {
         if (W > per_seg && W > 1) continue;
-        const uint32_t G = (per_seg + W - 1) / W;
-        if (G > MAX_G) continue;
+        uint32_t G = (per_seg + W - 1) / W;
+        if (wide_g(W, G)) {
+            G = (G + 3) / 4 * 4;
+            if (G > MAX_G_WIDE) continue;
+        } else if (G > MAX_G) {
+            continue;
+        }
         const uint32_t Wn = (per_seg + G - 1) / G;  // drop empty tail stages
         const size_t lds = lds_bytes(Wn, G, 2);
         if (lds > cap) continue;
@@ -964,10 +1010,11 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     // only decides how tight the candidate masks are)
     fp_thresholds(minc, maxc, a.tc);
     fp_thresholds(minm, maxm, a.tm);
-    if (G < 1 || G > MAX_G) return FP_EOVERFLOW;
+    const bool wide = wide_g(W, G);
+    if (G < 1 || (wide ? (G > MAX_G_WIDE || G % 4) : G > MAX_G)) return FP_EOVERFLOW;
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
-    int rc = kLaunch[G](st, (unsigned)(S * B), W * 64, lds, a);
+    int rc = (wide ? kLaunchWide[G / 4] : kLaunch[G])(st, (unsigned)(S * B), W * 64, lds, a);
     if (rc) return rc;
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);

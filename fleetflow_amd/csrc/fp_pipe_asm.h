@@ -145,15 +145,21 @@ __device__ __forceinline__ void fpp_asm_batch(uint64_t &todo, uint64_t &placed, 
 // moves the container to its next candidate group (nxt lane ti = first cand bit above g,
 // or G for none); a hit updates lane l of the records with v_writelane, clears the bucket
 // mask bits the placement crossed (one ds_mskor_b64) and records the assignment.
-//   q       lanes queued on g (consumed)       gb64   (gbase + g) * 64
-//   gbit    1 << g  (used-node bit)            nmask  ~((2 << g) - 1): candidate groups above g
-//   gnone   G (no further candidate)           maddr  LDS address of this lane's mask word of g
+// Every per-group constant is an immediate (the group index is a template parameter), so a
+// wide stage keeps no per-group scalars live:
+//   q       lanes queued on g (consumed)        gb64   gbase * 64 (SGPR); + g * 64 immediate
+//   G       groups per stage: "no further candidate"
+//   maddr   LDS address of this lane's mask word of group 0; + g * 512 as the ds offset
+template <uint32_t g, uint32_t G>
 __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint32_t &asg, uint32_t &used,
                                               uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
                                               uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
-                                              uint32_t cand, uint32_t my_t, uint32_t lsel, uint32_t maddr,
-                                              uint32_t gb64, uint32_t gbit, uint32_t nmask, uint32_t gnone,
-                                              uint32_t &nchk, uint32_t &nhit) {
+                                              uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lsel,
+                                              uint32_t maddr, uint32_t gb64, uint32_t &nchk, uint32_t &nhit) {
+    constexpr uint32_t gbit = 1u << (g & 31);                         // used-node bit (in used's word)
+    constexpr uint32_t nmask = g < 32 ? ~((2u << g) - 1u) : 0u;        // candidate groups above g
+    constexpr uint32_t nmask_hi = g < 32 ? 0xFFFFFFFFu : ~((2u << (g & 31)) - 1u);
+    constexpr uint32_t goff = g * 64u, moff = g * 512u;
     uint32_t ti, ccpu, cmem, creq, cconf, l, oc, om, ocu, ous, m0sv, t0, t1;
     uint64_t tbit, m, m2;
     asm volatile(
@@ -181,12 +187,19 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
         "v_cmp_eq_u32_e64 %[m2], 0, %[t0]\n\t"
         "s_and_b64 %[m], %[m], %[m2]\n\t"
         "s_cbranch_scc1 .Lfpg_hit%=\n\t"
-        // miss: the container's next candidate group (none: gnone)
+        // miss: the container's next candidate group (none: gnone); candidate groups are a
+        // 64-bit set in (cand, cand_hi)
         "v_readlane_b32 %[oc], %[cand], %[ti]\n\t"
+        "v_readlane_b32 %[ocu], %[candhi], %[ti]\n\t"
         "s_and_b32 %[oc], %[oc], %[nmask]\n\t"
+        "s_and_b32 %[ocu], %[ocu], %[nmaskhi]\n\t"
+        "s_ff1_i32_b32 %[ous], %[ocu]\n\t"
+        "s_add_u32 %[ous], %[ous], 32\n\t"
+        "s_cmp_eq_u32 %[ocu], 0\n\t"
+        "s_cselect_b32 %[ous], %[gnone], %[ous]\n\t"
         "s_ff1_i32_b32 %[om], %[oc]\n\t"
         "s_cmp_eq_u32 %[oc], 0\n\t"
-        "s_cselect_b32 %[om], %[gnone], %[om]\n\t"
+        "s_cselect_b32 %[om], %[ous], %[om]\n\t"
         "s_mov_b32 m0, %[ti]\n\t"
         "v_writelane_b32 %[nxt], %[om], m0\n\t"
         "s_cmp_lg_u64 %[q], 0\n\t"
@@ -219,9 +232,10 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
         "v_lshlrev_b64 v[80:81], %[l], v[82:83]\n\t"
         "v_cndmask_b32_e64 v80, 0, v80, %[m]\n\t"
         "v_cndmask_b32_e64 v81, 0, v81, %[m]\n\t"
-        "ds_mskor_b64 %[maddr], v[80:81], v[84:85]\n\t"
+        "ds_mskor_b64 %[maddr], v[80:81], v[84:85] offset:%[moff]\n\t"
         // assignment of lane ti: (gbase + g) * 64 + l
-        "s_or_b32 %[oc], %[gb64], %[l]\n\t"
+        "s_add_u32 %[oc], %[gb64], %[goff]\n\t"
+        "s_or_b32 %[oc], %[oc], %[l]\n\t"
         "s_mov_b32 m0, %[ti]\n\t"
         "v_writelane_b32 %[asg], %[oc], m0\n\t"
         "s_or_b64 %[placed], %[placed], %[tbit]\n\t"
@@ -235,9 +249,9 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
           [ti] "=&s"(ti), [ccpu] "=&s"(ccpu), [cmem] "=&s"(cmem), [creq] "=&s"(creq), [cconf] "=&s"(cconf),
           [l] "=&s"(l), [oc] "=&s"(oc), [om] "=&s"(om), [ocu] "=&s"(ocu), [ous] "=&s"(ous), [m0sv] "=&s"(m0sv),
           [tbit] "=&s"(tbit), [m] "=&s"(m), [m2] "=&s"(m2), [t0] "=&v"(t0), [t1] "=&v"(t1)
-        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [cand] "v"(cand),
-          [myt] "v"(my_t), [lsel] "v"(lsel), [maddr] "v"(maddr), [gb64] "s"(gb64), [gbit] "s"(gbit),
-          [nmask] "s"(nmask), [gnone] "s"(gnone)
+        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [cand] "v"(cand), [candhi] "v"(cand_hi),
+          [myt] "v"(my_t), [lsel] "v"(lsel), [maddr] "v"(maddr), [gb64] "s"(gb64), [gbit] "i"(gbit),
+          [nmask] "i"(nmask), [nmaskhi] "i"(nmask_hi), [gnone] "i"(G), [goff] "i"(goff), [moff] "i"(moff)
         : "scc", "memory", "v80", "v81", "v82", "v83", "v84", "v85");
 }
 

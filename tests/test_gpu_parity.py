@@ -486,10 +486,12 @@ def test_feasibility_random_vs_oracle(C, N, planner, O):
     assert np.array_equal(first, ef) and np.array_equal(count, ec) and np.array_equal(bm, eb)
 
 
-# ---- pipeline geometry: "wide" (segments of 40 groups, stages of 10) is what many
+# ---- pipeline geometry: "one-wave" (one-wave segments of up to 32 groups) is what many
 # scenarios get, "narrow" (segments of 4, stages of 1 group) what a few small ones get;
-# both are forced here so every size runs through both ------------------------------
-GEOMETRIES = {"wide": ("4", "40"), "narrow": ("4", "4"), "one-stage": ("1", "16")}
+# "wide" (4 stages of 10 groups) was round 1's many-scenario geometry, "one-wave-40" the
+# 64-bit group-set path (> 32 groups); all are forced here so every size runs through each
+GEOMETRIES = {"wide": ("4", "40"), "narrow": ("4", "4"), "one-stage": ("1", "16"), "one-wave": ("1", "32"),
+              "one-wave-40": ("1", "40")}
 
 
 @pytest.fixture(params=sorted(GEOMETRIES))
