@@ -203,9 +203,14 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
 }
 
 // BLK: 1024 for multi-stage segments (W <= 16 waves, <= 128 VGPRs each); 64 for the
-// one-wave segments of the wide geometry, whose 13..40 groups of records need up to 256 VGPRs
+// one-wave segments of the wide geometry, whose 13..40 groups of records take 4 VGPRs per
+// group.  FP_WIDE_WAVES = the waves per SIMD the one-wave kernels are compiled for (3: at
+// most 168 VGPRs, 12 segments in flight per CU)
+#ifndef FP_WIDE_WAVES
+#define FP_WIDE_WAVES 3
+#endif
 template <uint32_t G, uint32_t BLK>
-__global__ __launch_bounds__(BLK) void k_ffd_pipe(const PipeArgs a) {
+__global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = a.W, R = a.R, B = a.B;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -245,16 +250,25 @@ __global__ __launch_bounds__(BLK) void k_ffd_pipe(const PipeArgs a) {
     RecT<G> rcf, rmf, rcu, rlab;
     GM schedbits = 0;                                   // bit g: node (g, lane) schedulable
     uint32_t usedbits = 0, used_hi = 0;                 // bit g (g - 32 in used_hi): node (g, lane) used
+    {
+        // branch-free loads from one base address per array (group g at an immediate
+        // offset, padding lanes clamped to node 0): divergent per-group branches here kept
+        // 64-bit addresses of every group live at once and set the kernel's VGPR count
+        const uint32_t n0 = gbase * 64 + lane;
+        const uint32_t *cf0 = a.cf + nb + n0, *mf0 = a.mf + nb + n0, *cu0 = a.cu + nb + n0, *lb0 = a.lab + nb + n0;
+        const uint8_t *sc0 = a.sched + nb + n0;
 #pragma unroll
-    for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t n = (gbase + g) * 64 + lane;
-        const bool in = n < N;
-        const bool sc = in && a.sched[nb + n] != 0;
-        rcf[g] = sc ? a.cf[nb + n] : 0u;
-        rmf[g] = sc ? a.mf[nb + n] : 0u;
-        rcu[g] = sc ? a.cu[nb + n] : 0xFFFFFFFFu;
-        rlab[g] = sc ? ~a.lab[nb + n] : 0xFFFFFFFFu;
-        schedbits |= sc ? (GM(1) << g) : GM(0);
+        for (uint32_t g = 0; g < G; ++g) {
+            const bool in = n0 + g * 64 < N;
+            const int o = in ? (int)(g * 64) : -(int)n0;  // padding lanes read node 0 of the scenario
+            const bool sc = in && sc0[o] != 0;
+            const uint32_t x = cf0[o], y = mf0[o], z = cu0[o], l = lb0[o];
+            rcf[g] = sc ? x : 0u;
+            rmf[g] = sc ? y : 0u;
+            rcu[g] = sc ? z : 0xFFFFFFFFu;
+            rlab[g] = sc ? ~l : 0xFFFFFFFFu;
+            schedbits |= sc ? (GM(1) << g) : GM(0);
+        }
     }
     uint32_t zs_g = G, zs_l = 0;  // the tile's first schedulable node (all-zero containers)
 #pragma unroll
@@ -265,13 +279,17 @@ __global__ __launch_bounds__(BLK) void k_ffd_pipe(const PipeArgs a) {
             zs_l = (uint32_t)__builtin_ctzll(sm);
         }
     }
-    for (uint32_t g = 0; g < G; ++g) {
-        const bool sc = (schedbits >> g) & 1u;
-        const uint32_t x = rcf[g], y = rmf[g];
-        for (int k = 0; k < K; ++k) {  // every lane takes part in each ballot
-            const uint64_t bc = __builtin_amdgcn_ballot_w64(sc & (x >= __builtin_amdgcn_readlane(my_t, k)));
-            const uint64_t bm = __builtin_amdgcn_ballot_w64(sc & (y >= __builtin_amdgcn_readlane(my_t, K + k)));
-            if (lane == (uint32_t)k) {
+    // bucket-major (a rolled loop): two thresholds live in scalars at a time -- hoisting all
+    // 64 of them out of an unrolled loop spilled scalars into VGPR lanes
+#pragma unroll 1
+    for (uint32_t k = 0; k < (uint32_t)K; ++k) {
+        const uint32_t tc = __builtin_amdgcn_readlane(my_t, k), tm = __builtin_amdgcn_readlane(my_t, K + k);
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {  // every lane takes part in each ballot
+            const bool sc = (schedbits >> g) & 1u;
+            const uint64_t bc = __builtin_amdgcn_ballot_w64(sc & (rcf[g] >= tc));
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(sc & (rmf[g] >= tm));
+            if (lane == k) {
                 Mw[((size_t)g * K + k) * 2] = bc;
                 Mw[((size_t)g * K + k) * 2 + 1] = bm;
             }
@@ -914,10 +932,12 @@ bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint
     // placement frontier moves through them), so one wave does the same work in about the
     // same time while a scenario needs fewer registers than with 4-stage segments.
     const bool narrow = (uint64_t)S * NG <= kNarrowWaves;
-    // one-wave segments hold at most 32 groups: 28 groups take 233 VGPRs (two waves per
-    // SIMD), 36-40 groups spill
+    // one-wave segments hold at most 20 groups: 20 groups take 158 VGPRs, three waves per
+    // SIMD (FP_WIDE_WAVES), 12 segments in flight per CU.  Config 4 (5k nodes, 79 groups):
+    // 4 segments of 20 groups 56.7 ms, 3 of 28 groups 58.2 ms at three waves per SIMD
+    // (spilling) / 68.7 ms at two, 5 of 16 groups 64.1 ms.
     const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg
-                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : 32u;
+                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : 20u;
     const uint32_t B = (NG + seg_groups - 1) / seg_groups;
     const uint32_t per_seg = (NG + B - 1) / B;
     const uint32_t first_w = forced_w > 0 ? (uint32_t)forced_w : narrow ? 4u : 1u;
