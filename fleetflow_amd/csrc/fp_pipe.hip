@@ -801,7 +801,7 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
     const uint32_t total = S * C, stride = gridDim.x * blockDim.x;
     const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     for (size_t i0 = (size_t)lb * blockDim.x + threadIdx.x; i0 < total; i0 += 4 * (size_t)stride) {
-        uint32_t j[4], src[4], r[4], f[4], cy[4], cv[4], mv[4];
+        uint32_t j[4], src[4], r[4], f[4], cy[4], cv[4], mv[4], pos[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const size_t i = i0 + (size_t)u * stride;
@@ -811,7 +811,8 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
         for (int u = 0; u < 4; ++u) {
             const size_t i = i0 + (size_t)u * stride;
             if (i < total) {
-                src[u] = (uint32_t)i - (uint32_t)i % C + j[u];  // i < total < 2^32
+                pos[u] = (uint32_t)i % C;                        // sorted position in the scenario
+                src[u] = (uint32_t)i - pos[u] + j[u];            // i < total < 2^32
                 if (skeys) {
                     const uint64_t k = __builtin_nontemporal_load(&skeys[i]);
                     cv[u] = (uint32_t)(cmax - (mbits >= 64 ? 0ull : ((k >> mbits) & cmax)));
@@ -844,9 +845,49 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
                 __builtin_nontemporal_store(mv[u], &s_mem[i]);
                 __builtin_nontemporal_store(r[u], &s_req[i]);
                 __builtin_nontemporal_store(f[u], &s_conf[i]);
-                __builtin_nontemporal_store(j[u] | cy[u], &s_idx[i]);
+                // the pipeline carries the SORTED position: its assign/reason stores land
+                // next to each other (k_unsort restores container order, coalesced)
+                __builtin_nontemporal_store(pos[u] | cy[u], &s_idx[i]);
             }
         }
+    }
+}
+
+// assign/reason from FFD (sorted) order back to container order, per scenario and per
+// range of container indices held in LDS: every read and write is coalesced.  The
+// pipeline's stores hit the sorted arrays at positions that advance together, so its
+// partial lines merge in L2 instead of costing a 64-byte write each (round 1 wrote the
+// container-order arrays directly: 2.2 GB of WRITE_SIZE per 512-scenario launch for
+// 0.13 GB of outputs).
+// LDS holds a range of container indices per workgroup: 3 B per container (u16 node index,
+// u8 reason) when every node index fits 16 bits (N < 65535: one workgroup covers a config-4
+// scenario), 5 B otherwise.
+constexpr uint32_t UNSORT_SPAN16 = 50 * 1024;  // 150 KB of LDS
+constexpr uint32_t UNSORT_SPAN32 = 30 * 1024;  // 150 KB of LDS
+template <bool NARROW>
+__global__ __launch_bounds__(1024) void k_unsort(uint32_t C, uint32_t H, uint32_t span,
+                                                 const uint32_t *__restrict__ order,
+                                                 const uint32_t *__restrict__ asg_s, const uint8_t *__restrict__ rsn_s,
+                                                 uint32_t *__restrict__ assign, uint8_t *__restrict__ reason) {
+    using A = typename std::conditional<NARROW, uint16_t, uint32_t>::type;
+    extern __shared__ __attribute__((aligned(16))) unsigned char ulds[];
+    A *la = reinterpret_cast<A *>(ulds);
+    uint8_t *lr = ulds + (size_t)span * sizeof(A);
+    const uint32_t s = blockIdx.x / H, h = blockIdx.x % H;
+    const uint32_t lo = h * span, hi = min(C, lo + span);
+    const size_t cb = (size_t)s * C;
+    for (uint32_t p = threadIdx.x; p < C; p += blockDim.x) {
+        const uint32_t j = __builtin_nontemporal_load(&order[cb + p]);
+        if (j >= lo && j < hi) {
+            la[j - lo] = (A)__builtin_nontemporal_load(&asg_s[cb + p]);  // FP_NONE -> 0xFFFF when narrow
+            lr[j - lo] = __builtin_nontemporal_load(&rsn_s[cb + p]);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+        const A v = la[j - lo];
+        __builtin_nontemporal_store(NARROW && v == (A)0xFFFF ? FP_NONE : (uint32_t)v, &assign[cb + j]);
+        reason[cb + j] = lr[j - lo];
     }
 }
 
@@ -966,7 +1007,7 @@ size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
     size_t lds;
     if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return 0;
     const size_t SC = (size_t)S * C, nlinks = (size_t)S * (B - 1), slots = (C + 63) / 64 + 2;
-    return 5 * SC * 4 + 256 + nlinks * 128 + (size_t)S * B * 8 + 8 + nlinks * slots * 6 * 64 * 4 + 8 * 256;
+    return 5 * SC * 4 + SC * 5 + 256 + nlinks * 128 + (size_t)S * B * 8 + 8 + nlinks * slots * 6 * 64 * 4 + 10 * 256;
 }
 
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
@@ -999,7 +1040,9 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     uint32_t *ctl = (uint32_t *)fp_ws_take(c, 256 + nlinks * 128);  // ticket, abort | heads
     uint32_t *part = (uint32_t *)fp_ws_take(c, (size_t)S * B * 8 + 8);
     uint32_t *gdata = nlinks ? (uint32_t *)fp_ws_take(c, nlinks * slots * 6 * 64 * 4) : nullptr;
-    if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx || !ctl || !part || (nlinks && !gdata))
+    uint32_t *asg_s = (uint32_t *)fp_ws_take(c, SC * 4);  // plan in FFD order (k_unsort input)
+    uint8_t *rsn_s = (uint8_t *)fp_ws_take(c, SC);
+    if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx || !ctl || !part || (nlinks && !gdata) || !asg_s || !rsn_s)
         return FP_ENOMEM;
     FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * 128, st));
     {
@@ -1022,7 +1065,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.part = part;
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
-    a.assign = b->assign; a.reason = b->reason; a.cost = b->cost; a.err = c->d_err;
+    a.assign = asg_s; a.reason = rsn_s; a.cost = b->cost; a.err = c->d_err;
     a.spin_ticks = SPIN_TICKS;
     if (getenv("FLEETPLACE_SPIN_TICKS")) a.spin_ticks = strtoull(getenv("FLEETPLACE_SPIN_TICKS"), nullptr, 10);
     // thresholds: T0 = 0, then K-1 geometric steps from the smallest positive to
@@ -1038,6 +1081,19 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     if (rc) return rc;
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
+    {
+        const bool narrow16 = N < 0xFFFFu;  // node indices and FP_NONE (-> 0xFFFF) fit 16 bits
+        const uint32_t span = narrow16 ? UNSORT_SPAN16 : UNSORT_SPAN32;
+        const uint32_t H = (C + span - 1) / span;
+        const size_t ul = (size_t)span * (narrow16 ? 3 : 5);
+        const void *fn = narrow16 ? (const void *)k_unsort<true> : (const void *)k_unsort<false>;
+        FP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ul));
+        if (narrow16)
+            k_unsort<true><<<(unsigned)(S * H), 1024, ul, st>>>(C, H, span, order, asg_s, rsn_s, b->assign, b->reason);
+        else
+            k_unsort<false><<<(unsigned)(S * H), 1024, ul, st>>>(C, H, span, order, asg_s, rsn_s, b->assign, b->reason);
+        FP_HIP(hipGetLastError());
+    }
     if (b->cost) {
         k_cost_reduce<<<(S + 255) / 256, 256, 0, st>>>(S, B, scen_base, part, b->cost);
         FP_HIP(hipGetLastError());
