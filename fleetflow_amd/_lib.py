@@ -76,6 +76,7 @@ SIGNATURES = {
     "fp_dev_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), vp, vp, vp]),
     "fp_dev_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),
     "fp_dev_feasibility": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), vp, vp, vp]),
+    "fp_dev_feasibility_batch": (ct.c_int, [vp, ct.POINTER(FpBatch), vp, vp]),
     "fp_dev_argmin_cost": (ct.c_int, [vp, vp, ct.c_uint32, vp]),
     "fp_dev_gen_batch": (ct.c_int, [vp, ct.c_uint64, ct.POINTER(FpBatch), ct.c_uint32]),
 }

@@ -208,6 +208,11 @@ extern "C" int fp_dev_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm)
     FP_HIP(hipSetDevice(c->device));
     return fp_dev_legacy_order_impl(c, g, perm);
 }
+extern "C" int fp_dev_feasibility_batch(fp_ctx *c, const fp_batch *b, uint32_t *first, uint32_t *count) {
+    if (!c || !b) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_dev_feasibility_batch_impl(c, b, first, count);
+}
 extern "C" int fp_dev_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
                                   uint32_t *first, uint32_t *count, uint64_t *bitmap) {
     if (!c || !cs || !ns) return FP_EINVAL;

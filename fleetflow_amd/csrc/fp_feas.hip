@@ -20,6 +20,8 @@ struct alignas(16) NodeRec {
 
 struct FeasArgs {
     uint32_t C, N, WC, node_span;  // node_span: nodes per blockIdx.y (multiple of 64)
+    // scenario blockIdx.z: containers/outputs advance by C per scenario, nodes by N
+    // (fp_dev_feasibility_batch); 0 scenarios of stride for the single-scenario call
     const uint32_t *cpu, *mem, *req, *conf;
     const uint32_t *cf, *mf, *lab, *cu;
     const uint8_t *sched;
@@ -37,6 +39,11 @@ __global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
     __shared__ NodeRec rec[kTile];   // cf, mf, ~lab, cu
     __shared__ uint32_t sch[kTile];
     const uint32_t lane = threadIdx.x & 63;
+    if (gridDim.z > 1) {  // scenario blockIdx.z of a batch: rebase every array on it
+        const size_t sc = (size_t)blockIdx.z * a.C, sn = (size_t)blockIdx.z * a.N;
+        a.cpu += sc; a.mem += sc; a.req += sc; a.conf += sc; a.first += sc; a.count += sc;
+        a.cf += sn; a.mf += sn; a.lab += sn; a.cu += sn; a.sched += sn;
+    }
     uint32_t cpu[kPer], mem[kPer], req[kPer], conf[kPer], first[kPer], cnt[kPer], cidx[kPer];
     uint64_t word[kPer], cinm[kPer];
     bool cin[kPer];
@@ -106,6 +113,51 @@ __global__ __launch_bounds__(kBlock) void k_feas(FeasArgs a) {
 }
 
 }  // namespace
+
+// Stage 2 over S what-if scenarios at once (scenario-major SoA, fp_batch): per scenario and
+// container, the first feasible node and the number of feasible nodes on the scenario's node
+// state.  Same kernel as the single-scenario sweep, one grid z-slice per scenario.
+int fp_dev_feasibility_batch_impl(fp_ctx *c, const fp_batch *b, uint32_t *first, uint32_t *count) {
+    const uint32_t S = b->n_scen, C = b->n_containers, N = b->n_nodes;
+    if (S == 0 || C == 0) return FP_OK;
+    if (S > 65535u) return FP_EOVERFLOW;  // grid z
+    if (!b->cpu_m || !b->mem_mib || !b->req_labels || !b->conflict || !first || !count) return FP_EINVAL;
+    if (N && (!b->cpu_free || !b->mem_free || !b->labels || !b->conflict_used || !b->schedulable))
+        return FP_EINVAL;
+    hipStream_t st = c->stream;
+    const size_t SC = (size_t)S * C;
+    if (N == 0) {
+        FP_HIP(hipMemsetAsync(first, 0xFF, SC * 4, st));
+        FP_HIP(hipMemsetAsync(count, 0, SC * 4, st));
+        return FP_OK;
+    }
+    const uint32_t xb = (C + kBlock * kPer - 1) / (kBlock * kPer);
+    // split the node range only while the whole grid is small
+    uint32_t ysplit = 1;
+    const uint32_t max_split = (N + 63) / 64;
+    while ((uint64_t)xb * ysplit * S < 2048 && ysplit < max_split) ysplit *= 2;
+    if (ysplit > max_split) ysplit = max_split;
+    uint32_t span = (N + ysplit - 1) / ysplit;
+    span = (span + 63) & ~63u;
+    ysplit = (N + span - 1) / span;
+    FeasArgs a;
+    a.C = C; a.N = N; a.WC = (C + 63) / 64; a.node_span = span;
+    a.cpu = b->cpu_m; a.mem = b->mem_mib; a.req = b->req_labels; a.conf = b->conflict;
+    a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used;
+    a.sched = b->schedulable;
+    a.first = first; a.count = count; a.bitmap = nullptr;
+    a.split = ysplit > 1;  // node-range splits merge with atomics into memset outputs
+    if (a.split) {
+        FP_HIP(hipMemsetAsync(first, 0xFF, SC * 4, st));
+        FP_HIP(hipMemsetAsync(count, 0, SC * 4, st));
+    }
+    hipEvent_t ev;
+    fp_prof_begin(c, FP_K_FEAS, &ev);
+    k_feas<<<dim3(xb, ysplit, S), kBlock, 0, st>>>(a);
+    FP_HIP(hipGetLastError());
+    fp_prof_end(c, FP_K_FEAS, ev);
+    return FP_OK;
+}
 
 int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
                             uint32_t *first, uint32_t *count, uint64_t *bitmap) {

@@ -72,6 +72,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
 int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm);
 int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
                             uint32_t *first, uint32_t *count, uint64_t *bitmap);
+int fp_dev_feasibility_batch_impl(fp_ctx *c, const fp_batch *b, uint32_t *first, uint32_t *count);
 
 // tile-pipeline FFD (fp_pipe.hip)
 bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out);

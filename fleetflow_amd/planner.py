@@ -167,6 +167,11 @@ class Planner:
                                          count_t.data_ptr(), bitmap_t.data_ptr() if bitmap_t is not None else None),
               "fp_dev_feasibility")
 
+    def dev_feasibility_batch(self, db: "DevBatch", first_t, count_t):
+        """Stage 2 over every scenario of ``db`` ([S*C] outputs, scenario-major)."""
+        check(self._L.fp_dev_feasibility_batch(self._ctx, ct.byref(db.struct()), first_t.data_ptr(),
+                                               count_t.data_ptr()), "fp_dev_feasibility_batch")
+
     def dev_levelize(self, row_ptr_t, col_t, has_deps_t, level_t, order_t, ncyc_t):
         V = has_deps_t.numel()
         g = FpGraph(V, col_t.numel(), row_ptr_t.data_ptr(), col_t.data_ptr() if col_t.numel() else None,

@@ -15,6 +15,7 @@
  *                        (N = 1, unconstrained capacity reproduces it exactly)
  *   fp_place_batch    <- new: what-if scenarios, one plan per scenario + packed cost
  *   fp_feasibility    <- new: stage-2 containers x nodes feasibility/score sweep
+ *   fp_dev_feasibility_batch <- new: the same sweep over many what-if scenarios
  *
  * Conventions
  *   - All buffers are caller-owned; no allocation crosses the ABI.
@@ -146,6 +147,11 @@ int fp_dev_levelize(fp_ctx *ctx, const fp_graph *g, uint32_t *level_out, uint32_
 int fp_dev_place_batch(fp_ctx *ctx, const fp_batch *b);
 int fp_dev_feasibility(fp_ctx *ctx, const fp_containers *c, const fp_nodes *nodes,
                        uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out);
+/* Stage 2 batched over what-if scenarios: for each scenario s and container c of b
+ * (b's containers and node state; nothing is placed or mutated), first_out[s*C + c] = the
+ * lowest feasible node (FP_NONE if none) and count_out[s*C + c] = the number of feasible
+ * nodes.  n_scen <= 65535. */
+int fp_dev_feasibility_batch(fp_ctx *ctx, const fp_batch *b, uint32_t *first_out, uint32_t *count_out);
 /* Best plan over a cost vector (device): writes the argmin index to *best_dev. */
 int fp_dev_argmin_cost(fp_ctx *ctx, const uint64_t *cost, uint32_t n, uint32_t *best_dev);
 

@@ -552,3 +552,36 @@ def test_ffd_zero_demand_mixed(N, planner, O, geometry):
     _check_ffd(planner, O, (cpu, mem, req, conf), (cf, mf, lab, cu, sc))
     # nothing schedulable at all: zero containers are NOFIT too
     _check_ffd(planner, O, (cpu[:300], mem[:300], req[:300], conf[:300]), (cf, mf, lab, cu, np.zeros(N, np.uint8)))
+
+
+@pytest.mark.parametrize("S,C,N", [(3, 700, 300), (5, 3000, 5000), (4, 50_000, 5_000)])
+def test_feasibility_batch_vs_oracle(S, C, N, planner, O):
+    """Stage 2 batched over scenarios (fp_dev_feasibility_batch): every scenario's first
+    feasible node and feasible-node count equal the oracle's sweep on that scenario; the
+    node state is not mutated.  Half-used node states exercise the conflict/capacity tests."""
+    import torch
+    from fleetflow_amd import DevBatch
+    base = 11
+    db = DevBatch.allocate(S, C, N, "cuda:0", scen_base=base)
+    planner.dev_gen_batch(SEED + 6, db, 7)
+    rng = np.random.default_rng(S * C)
+    cu = torch.from_numpy(((rng.random(S * N) < 0.3).astype(np.uint32) << rng.integers(0, 32, S * N).astype(np.uint32))
+                          .view(np.int32)).to("cuda:0")
+    db.cu.copy_(cu)
+    db.cf.sub_(torch.from_numpy(rng.integers(0, 3000, S * N).astype(np.int32)).to("cuda:0")).clamp_(min=0)
+    snap = [t.clone() for t in (db.cf, db.mf, db.cu)]
+    first = torch.empty(S * C, dtype=torch.int32, device="cuda:0")
+    count = torch.empty(S * C, dtype=torch.int32, device="cuda:0")
+    planner.dev_feasibility_batch(db, first, count)
+    planner.sync()
+    assert all(torch.equal(a, b) for a, b in zip(snap, (db.cf, db.mf, db.cu)))
+    fh, ch = first.cpu().numpy().view(np.uint32), count.cpu().numpy().view(np.uint32)
+    nodes_all = [t.cpu().numpy() for t in (db.cf, db.mf, db.lab, db.cu, db.sched)]
+    for s in sorted({0, S // 2, S - 1}):
+        cont, _ = O.gen_scenario(SEED + 6, base + s, C, N, 7)
+        nodes = tuple(a[s * N:(s + 1) * N].view(np.uint32) if a.dtype != np.uint8 else a[s * N:(s + 1) * N]
+                      for a in nodes_all)
+        k = min(C, 4000)  # the oracle sweep is O(C*N): a prefix of the containers at full size
+        ef, ec, _ = O.feasibility(tuple(np.asarray(x)[:k] for x in cont), nodes, want_bitmap=False)
+        assert np.array_equal(fh[s * C:s * C + k], ef), s
+        assert np.array_equal(ch[s * C:s * C + k], ec), s

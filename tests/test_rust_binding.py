@@ -1,0 +1,114 @@
+"""The Rust crate's raw bindings (integration/fleetflow-placement/src/ffi.rs) must mirror
+include/fleetplace.h: every #[repr(C)] struct field for field (name, order, type), every
+declared function with the same parameter types, and the constants.  cargo is not in this
+image, so this is the layout check that a header change without a matching ffi.rs change
+fails ("a field reorder in the header would not fail any test")."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "fleetplace.h")
+FFI = os.path.join(ROOT, "integration", "fleetflow-placement", "src", "ffi.rs")
+
+C2R = {"uint32_t": "u32", "uint8_t": "u8", "uint64_t": "u64", "int": "c_int", "double": "f64", "void": "c_void",
+       "char": "c_char", "fp_ctx": "fp_ctx", "fp_graph": "fp_graph", "fp_containers": "fp_containers",
+       "fp_nodes": "fp_nodes", "fp_batch": "fp_batch"}
+
+
+def _strip_c(src):
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return re.sub(r"//[^\n]*", "", src)
+
+
+def c_type(base, const, stars):
+    t = C2R[base]
+    for i in range(stars):
+        t = ("*const " if (const and i == 0) else "*mut ") + t
+    return t
+
+
+def header_structs():
+    src = _strip_c(open(HDR).read())
+    out = {}
+    for body, name in re.findall(r"typedef struct\s*\{(.*?)\}\s*(\w+)\s*;", src, flags=re.S):
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            m = re.match(r"(const\s+)?(\w+)\s+(.*)", decl, flags=re.S)
+            const, base, rest = bool(m.group(1)), m.group(2), m.group(3)
+            for d in rest.split(","):
+                d = d.strip()
+                stars = d.count("*")
+                fields.append((d.replace("*", "").strip(), c_type(base, const, stars)))
+        out[name] = fields
+    return out
+
+
+def header_functions():
+    src = _strip_c(open(HDR).read())
+    out = {}
+    for ret, name, args in re.findall(r"\n\s*((?:const\s+)?\w+\s*\**)\s*(fp_\w+)\s*\(([^)]*)\)\s*;", src):
+        types = []
+        for a in args.split(","):
+            a = a.strip()
+            if not a or a == "void":
+                continue
+            m = re.match(r"(const\s+)?(\w+)\s*(\**)\s*\w*$", a)
+            types.append(c_type(m.group(2), bool(m.group(1)), len(m.group(3))))
+        out[name] = types
+    return out
+
+
+def rust_structs():
+    src = open(FFI).read()
+    out = {}
+    for name, body in re.findall(r"#\[repr\(C\)\]\s*pub struct (\w+)\s*\{(.*?)\}", src, flags=re.S):
+        body = re.sub(r"//[^\n]*", "", body)
+        out[name] = [(n, re.sub(r"\s+", " ", t).strip()) for n, t in re.findall(r"pub (\w+):\s*([^,]+),", body)]
+    return out
+
+
+def rust_functions():
+    src = open(FFI).read()
+    block = src[src.index("extern \"C\" {"):]
+    out = {}
+    for name, args in re.findall(r"pub fn (fp_\w+)\((.*?)\)", block, flags=re.S):
+        out[name] = [re.sub(r"\s+", " ", t).strip() for t in re.findall(r"\w+:\s*([^,]+)", args)]
+    return out
+
+
+def test_every_header_struct_is_mirrored_field_for_field():
+    hs, rs = header_structs(), rust_structs()
+    assert set(hs) == {"fp_graph", "fp_containers", "fp_nodes", "fp_batch"}
+    for name, fields in hs.items():
+        assert rs.get(name) == fields, (name, fields, rs.get(name))
+
+
+def test_every_header_function_is_bound_with_the_same_parameter_types():
+    hf, rf = header_functions(), rust_functions()
+    assert set(hf) == set(rf), (set(hf) ^ set(rf))
+    for name, types in hf.items():
+        got = [t.replace("f64", "f64") for t in rf[name]]
+        assert got == types, (name, types, got)
+
+
+def test_constants_match():
+    src = _strip_c(open(HDR).read())
+    rs = open(FFI).read()
+    for name, val in re.findall(r"#define (FP_E\w+|FP_OK|FP_ABI_VERSION)\s+\(?(-?\d+)\)?", src):
+        assert re.search(rf"pub const {name}: c_int = {val};", rs), name
+    assert "pub const FP_NONE: u32 = 0xFFFF_FFFF;" in rs
+    for name, val in re.findall(r"(FP_REASON_\w+) = (\d+)", src):
+        assert re.search(rf"pub const {name}: u8 = {val};", rs), name
+    for name, val in re.findall(r"(FP_K_(?!COUNT)\w+) = (\d+)", src):
+        assert re.search(rf"pub const {name}: c_int = {val};", rs), name
+
+
+def test_build_script_compiles_every_library_source():
+    mk = open(os.path.join(ROOT, "fleetflow_amd", "csrc", "Makefile")).read()
+    srcs = re.search(r"SRCS := (.*)", mk).group(1).split()
+    br = open(os.path.join(ROOT, "integration", "fleetflow-placement", "build.rs")).read()
+    listed = re.findall(r'"(fp_\w+\.hip)"', br)
+    assert sorted(listed) == sorted(srcs)
