@@ -24,7 +24,9 @@ the measured time with checks x cycles-per-check from the diagnostics build
 `work_equivalent`, labelled as what it is.
 
 A second leg, `config3`, times BASELINE configs[2] (1 scenario x 1M containers x
-100k nodes, the north-star sweep) on rank 0 at N = 1.
+100k nodes, the north-star sweep) on rank 0 at N = 1; a third, `stage2`, the
+scenario-batched feasibility/score sweep (fp_dev_feasibility_batch) against the
+VALU roofline.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -60,6 +62,7 @@ def parse():
     ap.add_argument("--scenarios", type=int, default=S4, help="total what-if scenarios (config 4: 4096)")
     ap.add_argument("--config3-steps", type=int, default=3)
     ap.add_argument("--no-config3", action="store_true")
+    ap.add_argument("--no-stage2", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0, help="CPU baseline sample budget (wall s)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads for the CPU baseline (default: min(16, usable cores); the GPU box grants 16/GPU)")
@@ -248,6 +251,56 @@ def config3_leg(planner, dev, steps, warmup):
     return out
 
 
+# VALU lane-operations per container x node evaluation in k_feas's inner loop (no bitmap):
+# 62 VALU instructions per 2 nodes x 4 containers per lane (hipcc -S of fp_feas.hip, gfx950)
+FEAS_VALU_PER_EVAL = 62 / 8
+# peak VALU lane-ops/s: 256 CUs x 4 SIMD x 32 lanes per cycle (wave64 issues over 2 cycles)
+# x 2.4 GHz (MI355X_MICROARCH.md)
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+
+
+def stage2_leg(planner, dev, steps, S=512):
+    """Stage 2 (north_star: 'coalesced containers-by-nodes feasibility and score sweep with
+    node-capacity tiles staged in LDS', batched over scenarios): fp_dev_feasibility_batch on
+    S config-4 scenarios' pristine node tables -- first feasible node + feasible-node count
+    for every (scenario, container).  VALU-bound (every evaluation is computed)."""
+    import torch
+
+    from fleetflow_amd import DevBatch
+    from fleetflow_amd._lib import FP_K_FEAS
+    db = DevBatch.allocate(S, C4, N4, dev)
+    planner.dev_gen_batch(SEED4, db, FLAGS)
+    first = torch.empty(S * C4, dtype=torch.int32, device=dev)
+    count = torch.empty(S * C4, dtype=torch.int32, device=dev)
+    planner.dev_feasibility_batch(db, first, count)
+    torch.cuda.synchronize(dev)
+    ref = count.clone()
+    planner.profile(True)
+    el = timed(steps, lambda: planner.dev_feasibility_batch(db, first, count),
+               lambda: torch.cuda.synchronize(dev), lambda: None)
+    planner.sync()
+    if not torch.equal(count, ref):
+        raise RuntimeError("stage 2: timed steps did not reproduce the warmup sweep")
+    k_ms, k_n = planner.kernel_stats(FP_K_FEAS)
+    planner.profile(False)
+    kernel_s = k_ms / max(k_n, 1) / 1e3
+    evals = S * C4 * N4
+    rate = evals / kernel_s
+    out = {"workload": f"stage-2 feasibility + score sweep, {S} config-4 scenarios x 50k containers x 5k nodes "
+                       "(fp_dev_feasibility_batch)",
+           "value": evals / (el / steps), "unit": "evals/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+           "kernel_ms": kernel_s * 1e3,
+           "roofline": {"bound": "valu", "achieved": rate * FEAS_VALU_PER_EVAL / 1e12,
+                        "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T lane-ops/s",
+                        "frac": rate * FEAS_VALU_PER_EVAL / VALU_PEAK_LANE_OPS,
+                        "valu_ops_per_eval": FEAS_VALU_PER_EVAL,
+                        "note": "every (container, node) pair is evaluated: node tiles are LDS-resident, so "
+                                "HBM traffic is ~16 B x (C + N) per scenario plus 8 B of outputs per container"}}
+    del db, first, count
+    torch.cuda.empty_cache()
+    return out
+
+
 def worker(args):
     if args.dry_launch:
         print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
@@ -348,6 +401,8 @@ def worker(args):
         torch.cuda.empty_cache()
         if not args.no_config3:
             out["config3"] = config3_leg(planner, dev, args.config3_steps, 1)
+        if not args.no_stage2:
+            out["stage2"] = stage2_leg(planner, dev, 3)
         if not args.no_cpu_baseline:
             try:
                 usable = len(os.sched_getaffinity(0))

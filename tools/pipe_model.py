@@ -24,12 +24,14 @@ import torch  # noqa: E402
 from fleetflow_amd import DevBatch, Planner, _lib  # noqa: E402
 
 # (leg, scenarios in the diagnostics run, C, N, seed, scenarios resident at once on 256 CUs)
-LEGS = [("config4", 512, 50_000, 5_000, 0x5EED0004, 512), ("config3", 1, 1_000_000, 100_000, 0x5EED0003, 1)]
+LEGS = [("config4", int(os.environ.get("S_DIAG", 768)), 50_000, 5_000, 0x5EED0004, 768),
+        ("config3", 1, 1_000_000, 100_000, 0x5EED0003, 1)]
 
 
 def measure(p, S, C, N, seed):
     db = DevBatch.allocate(S, C, N, "cuda:0")
     p.dev_gen_batch(seed, db, 7)
+    p.sync()  # the generator runs on the planner stream; torch copies on its own
     pristine = db.node_snapshot()
     torch.cuda.synchronize()
     L = _lib.load()
@@ -45,6 +47,7 @@ def measure(p, S, C, N, seed):
         p.dev_place_batch(db)
         p.sync()
     ms, n = p.kernel_stats(_lib.FP_K_PLACE)
+    print(f"  S={S} placed/scenario {int((db.reason == 0).sum().item()) / S:.0f}", flush=True)
     f(buf, 0)
     v = [[buf[w * 16 + i] for i in range(16)] for w in range(16)]
     v = [r for r in v if any(r)]

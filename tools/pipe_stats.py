@@ -22,6 +22,7 @@ def main():
     p = Planner(0)
     db = DevBatch.allocate(S, C, N, "cuda:0")
     p.dev_gen_batch(0x5EED0004, db, 7)
+    p.sync()  # the generator runs on the planner stream; torch copies on its own
     pristine = db.node_snapshot()
     torch.cuda.synchronize()
     L = _lib.load()
