@@ -77,10 +77,13 @@ int fp_dev_feasibility_batch_impl(fp_ctx *c, const fp_batch *b, uint32_t *first,
 // tile-pipeline FFD (fp_pipe.hip)
 bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out);
 size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N);
+// bucket thresholds of the candidate masks: K ascending values, T[0] = 0
+constexpr int FP_BUCKETS = 32;
+void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T);  // geometric from lo to hi
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
-                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b,
-                   uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm);
+                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
+                   const uint32_t *tm);
 
 // ---- device helpers ----
 namespace fpd {

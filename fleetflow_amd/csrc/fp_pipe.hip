@@ -32,6 +32,7 @@
 #endif
 #include "fp_pipe_asm.h"
 #include <stdlib.h>
+#include <string.h>
 #include <type_traits>
 #include <utility>
 
@@ -56,6 +57,7 @@ __device__ unsigned long long g_pipe_tl[16 * TL_B * 8];
 namespace fpp {
 
 constexpr int K = 32;               // threshold buckets per dimension
+static_assert(K == FP_BUCKETS, "fp_place.hip and the pipeline agree on the bucket count");
 constexpr uint32_t END = 0x80000000u;
 constexpr uint32_t CYC = 0x80000000u;
 // Deadlock guard: a wait longer than this (s_memrealtime runs at 100 MHz) aborts the
@@ -196,7 +198,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
         [&] {
             const uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
             if (q)
-                fpp_asm_group<gs, G>(q, placed, asg, gs < 32 ? used : used_hi, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs],
+                fpp_asm_group<gs, G, (G > 1)>(q, placed, asg, gs < 32 ? used : used_hi, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs],
                                      cpu, mem, req, conf, cand, cand_hi, my_t, lsel, maddr0, gb64, nchk, nhit);
         }(),
         ...);
@@ -313,6 +315,10 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
     uint32_t ohead = 0, ofill = 0, itail = 0, k0 = 0;
     uint32_t n_used = 0, n_rej = 0;
     uint32_t st_spin_in = 0, st_spin_out = 0, st_visits = 0, st_checks = 0, st_hits = 0, st_batches = 0;
+    // diagnostics (C++ loop, stats build): why candidate checks miss -- [0] cpu and mem fit some
+    // node (a label or conflict test failed), [1] cpu+mem+labels fit (conflict failed), [2] cpu
+    // fits some node but mem none, [3] mem fits some node but cpu none
+    uint32_t st_miss[4] = {0, 0, 0, 0};
     unsigned long long ck_in = 0, ck_pre = 0, ck_cand = 0, ck_fwd = 0, ck_wait = 0;
     const unsigned long long ck_t0 = STAT_CLK();
     unsigned long long ck_a, ck_b;
@@ -609,6 +615,15 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
                         const uint64_t ch = (uint32_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)cand >> 32), ti);
                         const uint64_t cc = ((ch << 32) | cl) & ~((2ull << g) - 1ull);
                         nxt = (uint32_t)fp_writelane((int)(cc ? (uint32_t)__builtin_ctzll(cc) : G), (int)ti, (int)nxt);
+                        if (STAT_ON) {
+                            const uint64_t mc = __builtin_amdgcn_ballot_w64(x >= c_cpu);
+                            const uint64_t mm = __builtin_amdgcn_ballot_w64(y >= c_mem);
+                            const uint64_t ml = __builtin_amdgcn_ballot_w64((rlab[g] & c_req) == 0u);
+                            st_miss[0] += (mc & mm) != 0;
+                            st_miss[1] += (mc & mm & ml) != 0;
+                            st_miss[2] += mc != 0 && !(mc & mm);
+                            st_miss[3] += mm != 0 && !(mc & mm);
+                        }
                     }
                 }
             }
@@ -739,15 +754,19 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         n_used = u;
     }
     if (lane == 0) {
+        // stats slot: global stage b * W + w when the scenario has at most 16, else w
+        const uint32_t st_slot = (B * W <= 16u) ? b * W + w : w;
+        (void)st_slot;
         atomicAdd(&CNT[0], n_used);
         atomicAdd(&CNT[1], n_rej);
-        STAT_ADD(w, 0, st_visits); STAT_ADD(w, 1, st_checks); STAT_ADD(w, 2, st_hits);
-        STAT_ADD(w, 3, st_batches); STAT_ADD(w, 4, st_spin_in); STAT_ADD(w, 5, st_spin_out);
-        STAT_ADD(w, 8, ck_in); STAT_ADD(w, 9, ck_pre); STAT_ADD(w, 10, ck_cand); STAT_ADD(w, 11, ck_fwd);
-        STAT_ADD(w, 12, ck_wait); STAT_ADD(w, 13, STAT_CLK() - ck_t0);
+        STAT_ADD(st_slot, 0, st_visits); STAT_ADD(st_slot, 1, st_checks); STAT_ADD(st_slot, 2, st_hits);
+        STAT_ADD(st_slot, 3, st_batches); STAT_ADD(st_slot, 4, st_spin_in); STAT_ADD(st_slot, 5, st_spin_out);
+        STAT_ADD(st_slot, 6, st_miss[0]); STAT_ADD(st_slot, 7, st_miss[1]); STAT_ADD(st_slot, 14, st_miss[2]); STAT_ADD(st_slot, 15, st_miss[3]);
+        STAT_ADD(st_slot, 8, ck_in); STAT_ADD(st_slot, 9, ck_pre); STAT_ADD(st_slot, 10, ck_cand); STAT_ADD(st_slot, 11, ck_fwd);
+        STAT_ADD(st_slot, 12, ck_wait); STAT_ADD(st_slot, 13, STAT_CLK() - ck_t0);
     }
     (void)ck_t0; (void)ck_in; (void)ck_pre; (void)ck_cand; (void)ck_fwd; (void)ck_wait;
-    (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
+    (void)st_miss; (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
     // write the tile's node state back (registers -> HBM)
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
@@ -927,7 +946,7 @@ static inline bool wide_g(uint32_t, uint32_t) { return false; }
 
 using namespace fpp;
 
-static void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
+void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
     T[0] = 0;
     if (lo == 0) lo = 1;
     if (hi < lo) hi = lo;
@@ -1012,7 +1031,8 @@ size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
 
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
-                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, uint32_t minc, uint32_t maxc, uint32_t minm, uint32_t maxm) {
+                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
+                   const uint32_t *tm) {
     uint32_t G, W, B;
     size_t lds;
     if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
@@ -1068,11 +1088,10 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.assign = asg_s; a.reason = rsn_s; a.cost = b->cost; a.err = c->d_err;
     a.spin_ticks = SPIN_TICKS;
     if (getenv("FLEETPLACE_SPIN_TICKS")) a.spin_ticks = strtoull(getenv("FLEETPLACE_SPIN_TICKS"), nullptr, 10);
-    // thresholds: T0 = 0, then K-1 geometric steps from the smallest positive to
-    // the largest demand of the batch (any ascending choice is exact; this one
-    // only decides how tight the candidate masks are)
-    fp_thresholds(minc, maxc, a.tc);
-    fp_thresholds(minm, maxm, a.tm);
+    // bucket thresholds (fp_place.hip chooses them; any ascending choice with T0 = 0 is
+    // exact -- it only decides how tight the candidate masks are)
+    memcpy(a.tc, tc, sizeof(a.tc));
+    memcpy(a.tm, tm, sizeof(a.tm));
     const bool wide = wide_g(W, G);
     if (G < 1 || (wide ? (G > MAX_G_WIDE || G % 4) : G > MAX_G)) return FP_EOVERFLOW;
     hipEvent_t ev;

@@ -233,6 +233,19 @@ __global__ void k_argmin_cost(const uint64_t *__restrict__ cost, uint32_t n, uin
 
 }  // namespace
 
+// T[0] = 0; T[1..31] spread evenly over the ascending distinct positive values v[0..d)
+// (every value is a threshold when there are at most 31)
+static void value_thresholds(const uint32_t *v, uint32_t d, uint32_t *T) {
+    while (d && v[0] == 0) { ++v; --d; }  // zero is T[0]
+    T[0] = 0;
+    for (int k = 1; k < FP_BUCKETS; ++k) {
+        if (d == 0) { T[k] = 1; continue; }
+        const uint64_t i = d <= (uint32_t)(FP_BUCKETS - 1) ? (uint64_t)(k - 1 < (int)d ? k - 1 : d - 1)
+                                                             : (uint64_t)(k - 1) * (d - 1) / (FP_BUCKETS - 2);
+        T[k] = v[i];
+    }
+}
+
 static inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;
     if (g > 65535u * 4) g = 65535u * 4;
@@ -385,9 +398,28 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     }
     fp_prof_end(c, FP_K_SORT, ev);
 
+    // ---- bucket thresholds of the pipeline's candidate masks ----
+    // With dense ranks the batch's distinct demand values are known (cval/mval): the
+    // thresholds are spread evenly over them, so every bucket spans about D / 31 distinct
+    // values (config 4: 79 cpu and 256 mem values -> 2.5 and 8 per bucket).  Geometric
+    // steps from min to max spanned 9 and 43 values per bucket at the top of the range,
+    // where most demands lie, and the loose buckets cost exact checks that miss.
+    // Otherwise (values >= 2^18): geometric from the smallest positive to the largest demand.
+    uint32_t tc[FP_BUCKETS], tm[FP_BUCKETS];
+    if (cval) {
+        std::vector<uint32_t> hv((size_t)dc + dm);
+        FP_HIP(hipMemcpyAsync(hv.data(), cval, (size_t)dc * 4, hipMemcpyDeviceToHost, st));
+        FP_HIP(hipMemcpyAsync(hv.data() + dc, mval, (size_t)dm * 4, hipMemcpyDeviceToHost, st));
+        FP_HIP(hipStreamSynchronize(st));
+        value_thresholds(hv.data(), dc, tc);
+        value_thresholds(hv.data() + dc, dm, tm);
+    } else {
+        fp_thresholds(minc == 0xFFFFFFFFu ? 1u : minc, maxc, tc);
+        fp_thresholds(minm == 0xFFFFFFFFu ? 1u : minm, maxm, tm);
+    }
+
     // ---- 4-5: placement + cost ----
-    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, cval, mval, b,
-                          minc == 0xFFFFFFFFu ? 1u : minc, maxc, minm == 0xFFFFFFFFu ? 1u : minm, maxm);
+    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, cval, mval, b, tc, tm);
 }
 
 extern "C" int fp_dev_argmin_cost(fp_ctx *c, const uint64_t *cost, uint32_t n, uint32_t *best) {

@@ -75,6 +75,11 @@ def main():
                     "cycles_per_check": cand / max(checks, 1), "cand_loop_cycles_per_scenario": cand,
                     "prescan_cycles_per_scenario": pre,
                     "stage_lifetime_cycles_summed_over_segments": life_sum,
+                    "miss_reasons_per_scenario": {"cap_ok_label_or_conflict": sum(r[6] for r in v) / S,
+                                                  "cap_label_ok_conflict": sum(r[7] for r in v) / S,
+                                                  "cpu_ok_mem_fails": sum(r[14] for r in v) / S,
+                                                  "mem_ok_cpu_fails": sum(r[15] for r in v) / S,
+                                                  "note": "C++ loop diagnostics build only (FP_NO_ASM)"},
                     "per_stage": [{"visits": r[0] / S, "checks": r[1] / S, "hits": r[2] / S,
                                    "cand_Mcycles": r[10] / S / 1e6, "prescan_Mcycles": r[9] / S / 1e6,
                                    "life_Mcycles": r[13] / S / 1e6} for r in v]}
