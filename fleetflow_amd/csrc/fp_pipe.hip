@@ -187,19 +187,46 @@ template <uint32_t G>
 using RecT = uint32_t[G];
 #endif
 
-// the group-major loop over a stage's groups, g a compile-time constant in every call
-template <uint32_t G, uint32_t... gs, class Rec>
+// the group-major loop over a stage's groups, g a compile-time constant in every call.
+// After a group's queue: the used-node bits and (UPD) the bucket masks catch up with the
+// nodes the queue placed on (`touched`), once per group and batch instead of per placement.
+// Bucket lane k (lanes 0-31 cpu thresholds, 32-63 mem) clears node l's bit when the node's
+// free capacity is now below the threshold.
+template <uint32_t G, bool UPD, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
-                                           uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lsel,
-                                           uint32_t maddr0, uint32_t gb64, uint32_t &nchk, uint32_t &nhit) {
+                                           uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
+                                           uint64_t *Mw, uint32_t gb64, uint32_t &nchk, uint32_t &nhit) {
     (
         [&] {
             const uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
-            if (q)
-                fpp_asm_group<gs, G, (G > 1)>(q, placed, asg, gs < 32 ? used : used_hi, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs],
-                                     cpu, mem, req, conf, cand, cand_hi, my_t, lsel, maddr0, gb64, nchk, nhit);
+            if (q) {
+                uint64_t touched = 0;
+                fpp_asm_group<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                                     req, conf, cand, cand_hi, gb64, nchk, nhit);
+                if (touched) {
+                    const bool me = (touched >> lane) & 1ull;
+                    if (gs < 32) used |= me ? (1u << gs) : 0u;
+                    else used_hi |= me ? (1u << (gs & 31)) : 0u;
+                    if (UPD) {
+                        uint64_t clr = 0, tt = touched;
+                        while (tt) {
+                            const uint32_t l = (uint32_t)__builtin_ctzll(tt);
+                            tt &= tt - 1;
+                            const uint32_t nc = __builtin_amdgcn_readlane(rcf[gs], l);
+                            const uint32_t nm = __builtin_amdgcn_readlane(rmf[gs], l);
+                            // a bit at or below the node's new free capacity stays; every bit above
+                            // it goes (clearing a bit that was already clear is harmless, so the
+                            // capacity before the queue is not needed)
+                            clr |= (my_t > (lane < 32 ? nc : nm)) ? (1ull << l) : 0ull;
+                        }
+                        if (__builtin_amdgcn_ballot_w64(clr != 0))
+                            atomicAnd((unsigned long long *)&Mw[(size_t)gs * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
+                                      ~clr);
+                    }
+                }
+            }
         }(),
         ...);
 }
@@ -565,14 +592,15 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         {
             uint32_t nxt = ((todo >> lane) & 1ull) ? (cand ? (uint32_t)__builtin_ctzll((uint64_t)cand) : G) : G;
 #ifndef FP_NO_ASM
-            // the hand-scheduled loop of fp_pipe_asm.h, one asm block per (static) group
-            const uint32_t lane_sel = lane < 32u ? 0xFFFFFFFFu : 0u;
-            const uint32_t maddr0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint64_t *)(
-                Mw + (lane & (K - 1)) * 2 + (lane >> 5));
+            // the hand-scheduled loop of fp_pipe_asm.h, one asm block per (static) group;
+            // one-group stages leave their bucket masks at the tile's start state (still
+            // exact: a stale mask is a superset): config 3 (1 x 1M x 100k) ran 127 -> 104 ms
+            // without the update, while config 4's 20-group stages need it (57 vs 66 ms)
             uint32_t nchk = 0, nhit = 0;
-            fpp_groups<G>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits, used_hi, rcf, rmf,
-                          rcu, rlab, cpu, mem, req, conf, (uint32_t)cand, (uint32_t)((uint64_t)cand >> 32), my_t,
-                          lane_sel, maddr0, __builtin_amdgcn_readfirstlane(gbase * 64u), nchk, nhit);
+            fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+                                   used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
+                                   (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
+                                   __builtin_amdgcn_readfirstlane(gbase * 64u), nchk, nhit);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
 #else
 #pragma unroll

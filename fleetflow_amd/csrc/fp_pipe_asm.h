@@ -137,58 +137,32 @@ __device__ __forceinline__ void fpp_asm_batch(uint64_t &todo, uint64_t &placed, 
           "v86", "v87");
 }
 
-// bucket masks (lanes 0-31 cpu, 32-63 mem): clear bit l where T <= old && T > new.
-// Without the update the masks keep their state from the tile's start: still exact (a
-// stale mask is a superset), at the price of more candidate checks that miss.  One-group
-// stages skip it (UPD = false): config 3 (1 x 1M x 100k) ran 127 -> 104 ms without the
-// update, config 4 (20-group one-wave segments) 57 -> 66 ms -- so the wide stages keep it.
-// -DFP_NO_MASK_UPDATE drops it everywhere (A/B).
-#define FPP_MASK_UPDATE_ASM                                               \
-    "v_mov_b32 %[t0], %[om]\n\t"                                        \
-    "v_bfi_b32 %[t0], %[lsel], %[oc], %[t0]\n\t"                        \
-    "v_mov_b32 %[t1], %[cmem]\n\t"                                      \
-    "v_bfi_b32 %[t1], %[lsel], %[ccpu], %[t1]\n\t"                      \
-    "v_cmp_le_u32_e64 %[m], %[myt], %[t0]\n\t"                          \
-    "v_cmp_gt_u32_e64 %[m2], %[myt], %[t1]\n\t"                         \
-    "s_and_b64 %[m], %[m], %[m2]\n\t"                                   \
-    "v_lshlrev_b64 v[80:81], %[l], v[82:83]\n\t"                        \
-    "v_cndmask_b32_e64 v80, 0, v80, %[m]\n\t"                           \
-    "v_cndmask_b32_e64 v81, 0, v81, %[m]\n\t"                           \
-    "ds_mskor_b64 %[maddr], v[80:81], v[84:85] offset:%[moff]\n\t"
-
 // Group-major candidate loop for ONE group g (the default build): exact first fit of the
-// containers queued on group g, in lane (= FFD) order.  Same checks and updates as
-// fpp_asm_batch, but the group's four records are plain "+v" operands -- the group index
-// is a compile-time constant of the caller, so there is no s_set_gpr_idx window and no
-// indexed copy: a check is 4 readlanes, 3 compares, 2 SALU ANDs and a branch.  A miss
-// moves the container to its next candidate group (nxt lane ti = first cand bit above g,
-// or G for none); a hit updates lane l of the records with v_writelane, clears the bucket
-// mask bits the placement crossed (one ds_mskor_b64) and records the assignment.
+// containers queued on group g, in lane (= FFD) order.  Same checks as fpp_asm_batch, but
+// the group's four records are plain "+v" operands -- the group index is a compile-time
+// constant of the caller, so there is no s_set_gpr_idx window and no indexed copy: a check
+// is 4 readlanes, 3 compares, 2 SALU ANDs and a branch.  A miss moves the container to its
+// next candidate group (nxt lane ti = first cand bit above g, or G for none); a hit updates
+// lane l of the records with v_writelane, records the assignment and sets bit l of
+// `touched`.  The bucket masks and the used-node bits are brought up to date once per
+// group and batch by the caller, from `touched` (off the per-placement chain).
 // Every per-group constant is an immediate (the group index is a template parameter), so a
 // wide stage keeps no per-group scalars live:
 //   q       lanes queued on g (consumed)        gb64   gbase * 64 (SGPR); + g * 64 immediate
 //   G       groups per stage: "no further candidate"
-//   maddr   LDS address of this lane's mask word of group 0; + g * 512 as the ds offset
-template <uint32_t g, uint32_t G, bool UPD>
-__device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint32_t &asg, uint32_t &used,
+template <uint32_t g, uint32_t G>
+__device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint64_t &touched, uint32_t &asg,
                                               uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
                                               uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
-                                              uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lsel,
-                                              uint32_t maddr, uint32_t gb64, uint32_t &nchk, uint32_t &nhit) {
-    constexpr uint32_t gbit = 1u << (g & 31);                         // used-node bit (in used's word)
+                                              uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
+                                              uint32_t &nhit) {
     constexpr uint32_t nmask = g < 32 ? ~((2u << g) - 1u) : 0u;        // candidate groups above g
     constexpr uint32_t nmask_hi = g < 32 ? 0xFFFFFFFFu : ~((2u << (g & 31)) - 1u);
-    constexpr uint32_t goff = g * 64u, moff = g * 512u;
-    uint32_t ti, ccpu, cmem, creq, cconf, l, oc, om, ocu, ous, m0sv, t0, t1;
+    constexpr uint32_t goff = g * 64u;
+    uint32_t ti, ccpu, cmem, creq, cconf, l, oc, om, ocu, ous, m0sv, t0;
     uint64_t tbit, m, m2;
-#ifndef FP_NO_MASK_UPDATE
-    if constexpr (UPD) {
     asm volatile(
         "s_mov_b32 %[m0sv], m0\n\t"
-        "v_mov_b32 v82, 1\n\t"
-        "v_mov_b32 v83, 0\n\t"
-        "v_mov_b32 v84, 0\n\t"
-        "v_mov_b32 v85, 0\n\t"
         "s_cmp_eq_u64 %[q], 0\n\t"
         "s_cbranch_scc1 .Lfpg_end%=\n"
         ".Lfpg_cont%=:\n\t"
@@ -208,7 +182,7 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
         "v_cmp_eq_u32_e64 %[m2], 0, %[t0]\n\t"
         "s_and_b64 %[m], %[m], %[m2]\n\t"
         "s_cbranch_scc1 .Lfpg_hit%=\n\t"
-        // miss: the container's next candidate group (none: gnone); candidate groups are a
+        // miss: the container's next candidate group (none: G); candidate groups are a
         // 64-bit set in (cand, cand_hi)
         "v_readlane_b32 %[oc], %[cand], %[ti]\n\t"
         "v_readlane_b32 %[ocu], %[candhi], %[ti]\n\t"
@@ -232,17 +206,15 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
         "v_readlane_b32 %[oc], %[rcf], %[l]\n\t"
         "v_readlane_b32 %[om], %[rmf], %[l]\n\t"
         "v_readlane_b32 %[ocu], %[rcu], %[l]\n\t"
-        "v_readlane_b32 %[ous], %[used], %[l]\n\t"
         "s_mov_b32 m0, %[l]\n\t"
         "s_sub_u32 %[ccpu], %[oc], %[ccpu]\n\t"    // new cpu_free
         "s_sub_u32 %[cmem], %[om], %[cmem]\n\t"    // new mem_free
         "s_or_b32 %[ocu], %[ocu], %[cconf]\n\t"    // new conflict_used
-        "s_or_b32 %[ous], %[ous], %[gbit]\n\t"     // node used
         "v_writelane_b32 %[rcf], %[ccpu], m0\n\t"
         "v_writelane_b32 %[rmf], %[cmem], m0\n\t"
         "v_writelane_b32 %[rcu], %[ocu], m0\n\t"
-        "v_writelane_b32 %[used], %[ous], m0\n\t"
-        FPP_MASK_UPDATE_ASM
+        "s_lshl_b64 %[m2], 1, %[l]\n\t"
+        "s_or_b64 %[touched], %[touched], %[m2]\n\t"
         // assignment of lane ti: (gbase + g) * 64 + l
         "s_add_u32 %[oc], %[gb64], %[goff]\n\t"
         "s_or_b32 %[oc], %[oc], %[l]\n\t"
@@ -252,100 +224,16 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
         "s_cmp_lg_u64 %[q], 0\n\t"
         "s_cbranch_scc1 .Lfpg_cont%=\n"
         ".Lfpg_end%=:\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
         "s_mov_b32 m0, %[m0sv]"
-        : [q] "+s"(q), [placed] "+s"(placed), [asg] "+v"(asg), [used] "+v"(used), [nxt] "+v"(nxt),
+        : [q] "+s"(q), [placed] "+s"(placed), [touched] "+s"(touched), [asg] "+v"(asg), [nxt] "+v"(nxt),
           [rcf] "+v"(rcf), [rmf] "+v"(rmf), [rcu] "+v"(rcu), [nchk] "+s"(nchk), [nhit] "+s"(nhit),
           [ti] "=&s"(ti), [ccpu] "=&s"(ccpu), [cmem] "=&s"(cmem), [creq] "=&s"(creq), [cconf] "=&s"(cconf),
           [l] "=&s"(l), [oc] "=&s"(oc), [om] "=&s"(om), [ocu] "=&s"(ocu), [ous] "=&s"(ous), [m0sv] "=&s"(m0sv),
-          [tbit] "=&s"(tbit), [m] "=&s"(m), [m2] "=&s"(m2), [t0] "=&v"(t0), [t1] "=&v"(t1)
-        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [cand] "v"(cand), [candhi] "v"(cand_hi),
-          [myt] "v"(my_t), [lsel] "v"(lsel), [maddr] "v"(maddr), [gb64] "s"(gb64), [gbit] "i"(gbit),
-          [nmask] "i"(nmask), [nmaskhi] "i"(nmask_hi), [gnone] "i"(G), [goff] "i"(goff), [moff] "i"(moff)
-        : "scc", "memory", "v80", "v81", "v82", "v83", "v84", "v85");
-    } else
-#endif
-    {
-    asm volatile(
-        "s_mov_b32 %[m0sv], m0\n\t"
-        "v_mov_b32 v82, 1\n\t"
-        "v_mov_b32 v83, 0\n\t"
-        "v_mov_b32 v84, 0\n\t"
-        "v_mov_b32 v85, 0\n\t"
-        "s_cmp_eq_u64 %[q], 0\n\t"
-        "s_cbranch_scc1 .Lfpg_end%=\n"
-        ".Lfpg_cont%=:\n\t"
-        "s_ff1_i32_b64 %[ti], %[q]\n\t"
-        "s_lshl_b64 %[tbit], 1, %[ti]\n\t"
-        "s_andn2_b64 %[q], %[q], %[tbit]\n\t"
-        "v_readlane_b32 %[ccpu], %[cpu], %[ti]\n\t"
-        "v_readlane_b32 %[cmem], %[mem], %[ti]\n\t"
-        "v_readlane_b32 %[creq], %[req], %[ti]\n\t"
-        "v_readlane_b32 %[cconf], %[conf], %[ti]\n\t"
-        FPP_ASM_CNT_CHECK
-        "v_cmp_ge_u32_e64 %[m], %[rcf], %[ccpu]\n\t"
-        "v_cmp_ge_u32_e64 %[m2], %[rmf], %[cmem]\n\t"
-        "v_and_b32_e32 %[t0], %[creq], %[rlab]\n\t"
-        "v_and_or_b32 %[t0], %[rcu], %[cconf], %[t0]\n\t"
-        "s_and_b64 %[m], %[m], %[m2]\n\t"
-        "v_cmp_eq_u32_e64 %[m2], 0, %[t0]\n\t"
-        "s_and_b64 %[m], %[m], %[m2]\n\t"
-        "s_cbranch_scc1 .Lfpg_hit%=\n\t"
-        // miss: the container's next candidate group (none: gnone); candidate groups are a
-        // 64-bit set in (cand, cand_hi)
-        "v_readlane_b32 %[oc], %[cand], %[ti]\n\t"
-        "v_readlane_b32 %[ocu], %[candhi], %[ti]\n\t"
-        "s_and_b32 %[oc], %[oc], %[nmask]\n\t"
-        "s_and_b32 %[ocu], %[ocu], %[nmaskhi]\n\t"
-        "s_ff1_i32_b32 %[ous], %[ocu]\n\t"
-        "s_add_u32 %[ous], %[ous], 32\n\t"
-        "s_cmp_eq_u32 %[ocu], 0\n\t"
-        "s_cselect_b32 %[ous], %[gnone], %[ous]\n\t"
-        "s_ff1_i32_b32 %[om], %[oc]\n\t"
-        "s_cmp_eq_u32 %[oc], 0\n\t"
-        "s_cselect_b32 %[om], %[ous], %[om]\n\t"
-        "s_mov_b32 m0, %[ti]\n\t"
-        "v_writelane_b32 %[nxt], %[om], m0\n\t"
-        "s_cmp_lg_u64 %[q], 0\n\t"
-        "s_cbranch_scc1 .Lfpg_cont%=\n\t"
-        "s_branch .Lfpg_end%=\n"
-        ".Lfpg_hit%=:\n\t"
-        FPP_ASM_CNT_HIT
-        "s_ff1_i32_b64 %[l], %[m]\n\t"
-        "v_readlane_b32 %[oc], %[rcf], %[l]\n\t"
-        "v_readlane_b32 %[om], %[rmf], %[l]\n\t"
-        "v_readlane_b32 %[ocu], %[rcu], %[l]\n\t"
-        "v_readlane_b32 %[ous], %[used], %[l]\n\t"
-        "s_mov_b32 m0, %[l]\n\t"
-        "s_sub_u32 %[ccpu], %[oc], %[ccpu]\n\t"    // new cpu_free
-        "s_sub_u32 %[cmem], %[om], %[cmem]\n\t"    // new mem_free
-        "s_or_b32 %[ocu], %[ocu], %[cconf]\n\t"    // new conflict_used
-        "s_or_b32 %[ous], %[ous], %[gbit]\n\t"     // node used
-        "v_writelane_b32 %[rcf], %[ccpu], m0\n\t"
-        "v_writelane_b32 %[rmf], %[cmem], m0\n\t"
-        "v_writelane_b32 %[rcu], %[ocu], m0\n\t"
-        "v_writelane_b32 %[used], %[ous], m0\n\t"
-        // assignment of lane ti: (gbase + g) * 64 + l
-        "s_add_u32 %[oc], %[gb64], %[goff]\n\t"
-        "s_or_b32 %[oc], %[oc], %[l]\n\t"
-        "s_mov_b32 m0, %[ti]\n\t"
-        "v_writelane_b32 %[asg], %[oc], m0\n\t"
-        "s_or_b64 %[placed], %[placed], %[tbit]\n\t"
-        "s_cmp_lg_u64 %[q], 0\n\t"
-        "s_cbranch_scc1 .Lfpg_cont%=\n"
-        ".Lfpg_end%=:\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_mov_b32 m0, %[m0sv]"
-        : [q] "+s"(q), [placed] "+s"(placed), [asg] "+v"(asg), [used] "+v"(used), [nxt] "+v"(nxt),
-          [rcf] "+v"(rcf), [rmf] "+v"(rmf), [rcu] "+v"(rcu), [nchk] "+s"(nchk), [nhit] "+s"(nhit),
-          [ti] "=&s"(ti), [ccpu] "=&s"(ccpu), [cmem] "=&s"(cmem), [creq] "=&s"(creq), [cconf] "=&s"(cconf),
-          [l] "=&s"(l), [oc] "=&s"(oc), [om] "=&s"(om), [ocu] "=&s"(ocu), [ous] "=&s"(ous), [m0sv] "=&s"(m0sv),
-          [tbit] "=&s"(tbit), [m] "=&s"(m), [m2] "=&s"(m2), [t0] "=&v"(t0), [t1] "=&v"(t1)
-        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [cand] "v"(cand), [candhi] "v"(cand_hi),
-          [myt] "v"(my_t), [lsel] "v"(lsel), [maddr] "v"(maddr), [gb64] "s"(gb64), [gbit] "i"(gbit),
-          [nmask] "i"(nmask), [nmaskhi] "i"(nmask_hi), [gnone] "i"(G), [goff] "i"(goff), [moff] "i"(moff)
-        : "scc", "memory", "v80", "v81", "v82", "v83", "v84", "v85");
-    }
+          [tbit] "=&s"(tbit), [m] "=&s"(m), [m2] "=&s"(m2), [t0] "=&v"(t0)
+        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [cand] "v"(cand),
+          [candhi] "v"(cand_hi), [gb64] "s"(gb64), [nmask] "i"(nmask), [nmaskhi] "i"(nmask_hi), [gnone] "i"(G),
+          [goff] "i"(goff)
+        : "scc", "memory");
 }
 
 }  // namespace fpp
