@@ -192,15 +192,49 @@ using RecT = uint32_t[G];
 // nodes the queue placed on (`touched`), once per group and batch instead of per placement.
 // Bucket lane k (lanes 0-31 cpu thresholds, 32-63 mem) clears node l's bit when the node's
 // free capacity is now below the threshold.
+//
+// Queue prefilter: group g's records do not change before its queue is processed, so a
+// queued container that fits no node of g NOW never will (monotone) and leaves for its
+// next candidate group without a serial check.  The test is vector-parallel over the
+// queue: the nodes that could take the batch's smallest demands (the batch corner, qc/qm)
+// are broadcast one at a time and every lane tests its own container.  It pays while the
+// corner holds few nodes (the filled-up frontier group); above FP_PF_MAX nodes the queue
+// goes to the serial loop unfiltered.
+#ifndef FP_PF_MAX
+#define FP_PF_MAX 16
+#endif
 template <uint32_t G, bool UPD, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
-                                           uint64_t *Mw, uint32_t gb64, uint32_t &nchk, uint32_t &nhit) {
+                                           uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
+                                           uint32_t &nhit) {
     (
         [&] {
-            const uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
+            uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
+            if (FP_PF_MAX > 0 && q) {
+                uint64_t e = __builtin_amdgcn_ballot_w64((rcf[gs] >= qc) & (rmf[gs] >= qm));
+                if (__builtin_popcountll(e) <= FP_PF_MAX) {
+                    bool ok = false;
+                    while (e) {
+                        const uint32_t l = (uint32_t)__builtin_ctzll(e);
+                        e &= e - 1;
+                        const uint32_t ncf = __builtin_amdgcn_readlane(rcf[gs], l);
+                        const uint32_t nmf = __builtin_amdgcn_readlane(rmf[gs], l);
+                        const uint32_t nlb = __builtin_amdgcn_readlane(rlab[gs], l);
+                        const uint32_t ncu = __builtin_amdgcn_readlane(rcu[gs], l);
+                        ok |= (ncf >= cpu) & (nmf >= mem) & (((req & nlb) | (conf & ncu)) == 0u);
+                    }
+                    const uint64_t fit = q & __builtin_amdgcn_ballot_w64(ok);
+                    if (q != fit) {  // the others move on: next candidate group above g, or none
+                        const uint64_t above = (((uint64_t)cand_hi << 32) | cand) & ~((2ull << gs) - 1ull);
+                        const uint32_t nx = above ? (uint32_t)__builtin_ctzll(above) : G;
+                        nxt = ((q & ~fit) >> lane) & 1ull ? nx : nxt;
+                    }
+                    q = fit;
+                }
+            }
             if (q) {
                 uint64_t touched = 0;
                 fpp_asm_group<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
@@ -600,7 +634,7 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                    used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                    (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
-                                   __builtin_amdgcn_readfirstlane(gbase * 64u), nchk, nhit);
+                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
 #else
 #pragma unroll
