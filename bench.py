@@ -35,7 +35,6 @@ any GPU call in this parent), one per GPU, over torch.distributed (RCCL).
 """
 import argparse
 import json
-import math
 import os
 import socket
 import statistics
@@ -190,10 +189,12 @@ def roofline(leg, S, C, N, kernel_s, step_s):
                                "GBps": 16 * S * C * N / kernel_s / 1e9}}
     m = (_load_json(MODEL_FILE) or {}).get(leg)
     if m and m.get("C") == C and m.get("N") == N:
-        rounds = math.ceil(S / m["resident_scenarios"])
-        model_ms = rounds * m["chain_cycles_per_scenario"] / (m["clock_ghz"] * 1e6)
-        out["latency_model"] = dict(m, rounds=rounds, model_ms=model_ms, measured_kernel_ms=kernel_s * 1e3,
-                                    formula="ceil(S / resident_scenarios) x chain_cycles_per_scenario / clock")
+        lm = dict(m, measured_kernel_ms=kernel_s * 1e3)
+        if "slot_cycles_per_scenario" in m:
+            lm["model_ms"] = S * m["slot_cycles_per_scenario"] / m["slots"] / (m["clock_ghz"] * 1e6)
+        if traffic:
+            lm["hbm_time_at_peak_ms"] = traffic / (HBM_PEAK_GBPS * 1e9) * 1e3
+        out["latency_model"] = lm
     return out
 
 
