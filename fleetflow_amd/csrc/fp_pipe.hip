@@ -73,6 +73,8 @@ constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
 struct PipeArgs {
     uint32_t C, N, scen_base, W, G, R;
     uint32_t B;       // segments (workgroups) per scenario
+    uint32_t S;       // scenarios of the launch
+    uint32_t lag;     // ticket lag between consecutive segments of a scenario (see the kernel)
     uint32_t slots;   // slots per global link (every container fits: never blocks)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
@@ -289,14 +291,32 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
 
     for (uint32_t i = threadIdx.x; i < (W - 1) * 8 + 8; i += blockDim.x) CTL[i] = 0;
     __syncthreads();
-    // Ticket order = start order: segment b of a scenario only ever waits on
-    // segments < b, which took earlier tickets, are already running, and never wait
-    // on b (global links are sized for every container) -- so the chain makes
-    // progress whatever the residency or dispatch order.
-    if (threadIdx.x == 0) CNT[4] = atomicAdd(a.ticket, 1u);
+    // Ticket order = start order.  Ticket t is round r = t / B, segment b = t % B, and
+    // scenario s = r - b * lag: segment b of scenario s starts `lag` rounds after segment
+    // b - 1 of it.  Segment b only ever waits on segment b - 1, which took an earlier
+    // ticket, is running or done, and never waits on b (global links hold every
+    // container) -- so the chain progresses whatever the residency or dispatch order.
+    // lag = 0 runs a scenario's segments side by side (one scenario: the pipeline is all
+    // the parallelism there is); with many scenarios a lag of about the resident
+    // segment count starts a segment when its input is (nearly) complete, so it is busy
+    // for its whole lifetime instead of waiting on its upstream half the time.
+    // Tickets naming no scenario (the ramp at either end) are skipped; a workgroup
+    // that finds none left exits.
+    if (threadIdx.x == 0) {
+        const uint32_t total = (a.S + (B - 1) * a.lag) * B;
+        uint32_t t;
+        while (true) {
+            t = atomicAdd(a.ticket, 1u);
+            if (t >= total) { t = 0xFFFFFFFFu; break; }
+            const uint32_t r = t / B, bb = t % B;
+            if (r >= bb * a.lag && r - bb * a.lag < a.S) break;
+        }
+        CNT[4] = t;
+    }
     __syncthreads();
     const uint32_t tk = __builtin_amdgcn_readfirstlane(CNT[4]);
-    const uint32_t s = tk / B, b = tk % B;
+    if (tk == 0xFFFFFFFFu) return;  // uniform: every wave of the workgroup leaves
+    const uint32_t b = tk % B, s = tk / B - b * a.lag;
     const size_t cb = (size_t)s * C, nb = (size_t)s * N;
 
     // ---- stage the tile into LDS and build the bucket masks ----
@@ -987,6 +1007,14 @@ static int launch_g(hipStream_t st, unsigned grid, unsigned block, size_t lds, c
 }
 
 typedef int (*launch_fn)(hipStream_t, unsigned, unsigned, size_t, const PipeArgs &);
+// the kernels themselves (occupancy queries)
+static const void *const kKernel[MAX_G + 1] = {
+    nullptr, (const void *)k_ffd_pipe<1, 1024>, (const void *)k_ffd_pipe<2, 1024>, (const void *)k_ffd_pipe<3, 1024>,
+    (const void *)k_ffd_pipe<4, 1024>, (const void *)k_ffd_pipe<5, 1024>, (const void *)k_ffd_pipe<6, 1024>,
+    (const void *)k_ffd_pipe<7, 1024>, (const void *)k_ffd_pipe<8, 1024>, (const void *)k_ffd_pipe<9, 1024>,
+    (const void *)k_ffd_pipe<10, 1024>, (const void *)k_ffd_pipe<11, 1024>, (const void *)k_ffd_pipe<12, 1024>,
+    (const void *)k_ffd_pipe<13, 1024>, (const void *)k_ffd_pipe<14, 1024>, (const void *)k_ffd_pipe<15, 1024>,
+    (const void *)k_ffd_pipe<16, 1024>};
 static const launch_fn kLaunch[MAX_G + 1] = {
     nullptr,         launch_g<1>,  launch_g<2>,  launch_g<3>,  launch_g<4>,  launch_g<5>,
     launch_g<6>,     launch_g<7>,  launch_g<8>,  launch_g<9>,  launch_g<10>, launch_g<11>,
@@ -998,9 +1026,14 @@ constexpr uint32_t MAX_G_WIDE = 40;
 static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {
     nullptr, nullptr, nullptr, nullptr, launch_g<16, 64>, launch_g<20, 64>,
     launch_g<24, 64>, launch_g<28, 64>, launch_g<32, 64>, launch_g<36, 64>, launch_g<40, 64>};
+static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {
+    nullptr, nullptr, nullptr, nullptr, (const void *)k_ffd_pipe<16, 64>, (const void *)k_ffd_pipe<20, 64>,
+    (const void *)k_ffd_pipe<24, 64>, (const void *)k_ffd_pipe<28, 64>, (const void *)k_ffd_pipe<32, 64>,
+    (const void *)k_ffd_pipe<36, 64>, (const void *)k_ffd_pipe<40, 64>};
 static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G > 12; }
 #else  // round 1's loops take at most 16 groups per stage
 static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {nullptr};
+static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {nullptr};
 static inline bool wide_g(uint32_t, uint32_t) { return false; }
 #endif
 
@@ -1144,6 +1177,24 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     PipeArgs a;
     a.C = C; a.N = N; a.scen_base = scen_base; a.W = W; a.G = G; a.R = R;
     a.B = B; a.slots = slots; a.ticket = ctl; a.gabort = ctl + 32; a.ghead = ctl + 64; a.gdata = gdata;
+    a.S = S;
+    // segment lag (kernel comment): twice the resident segments per segment index when
+    // there are enough scenarios, else 0.  FLEETPLACE_PIPE_LAG overrides (A/B, tests).
+    a.lag = 0;
+    if (B > 1 && S > 1) {
+        int dev_cu = 0, occ = 0;
+        (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+        const bool wide = wide_g(W, G);
+        const void *fn = wide ? kKernelWide[G / 4] : kKernel[G];
+        if (fn && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), lds) == hipSuccess && occ > 0) {
+            const uint64_t slots_total = (uint64_t)occ * (uint64_t)(dev_cu > 0 ? dev_cu : 1);
+            // config 4 (3072 slots, 4 segments): lag 768 ran the FFD kernel in 31.7 ms, 1536 in
+            // 30.1, 256 in 37.1, 0 in 50.9
+            const uint64_t lag = 2 * slots_total / B;
+            a.lag = (uint32_t)(lag < S ? lag : S);
+        }
+    }
+    if (getenv("FLEETPLACE_PIPE_LAG")) a.lag = (uint32_t)atoi(getenv("FLEETPLACE_PIPE_LAG"));
     a.part = part;
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
