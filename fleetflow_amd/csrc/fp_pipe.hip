@@ -79,7 +79,7 @@ struct PipeArgs {
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
     uint32_t *ghead;  // [S][B-1] link heads, 128 B apart
-    uint32_t *gdata;  // [S][B-1][slots][6][64] link slots: row 0 = count, rows 1..5 = fields
+    uint32_t *gdata;  // [S][B-1][slots][2][64] link slots: row 0 = count, row 1 = FFD positions
     uint32_t *part;   // [S][B][2] per-segment (n_used, n_rej)
     const uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;  // FFD-sorted SoA [S][C]; idx bit31 = CYCLE
     uint32_t *cf, *mf;
@@ -383,7 +383,10 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
     const bool has_out = w + 1 < W;
     const bool g_in = w == 0 && b > 0;                  // input from segment b-1
     const bool g_out = w + 1 == W && b + 1 < B;         // output to segment b+1
-    const size_t LSLOT = 6 * 64;                        // u32 per global slot
+    // a global link slot: [0] = count (or END), [64..127] = the containers' FFD positions;
+    // the consumer re-reads their fields from the sorted SoA (4 B per forwarded container
+    // instead of 20: links sized for every container stay 5x smaller)
+    const size_t LSLOT = 2 * 64;                        // u32 per global slot
     uint32_t *gin_head = a.ghead + ((size_t)s * (B - 1) + (b - 1)) * 32;
     uint32_t *gin_data = a.gdata + ((size_t)s * (B - 1) + (b - 1)) * a.slots * LSLOT;
     uint32_t *gout_head = a.ghead + ((size_t)s * (B - 1) + b) * 32;
@@ -435,14 +438,15 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
             const uint32_t *sd = gin_data + (size_t)itail * LSLOT;
             const uint32_t n = g_ld(sd);
+            const uint32_t pos = g_ld(sd + 64 + lane);  // with the count: one round trip
             if (n & END) break;
             valid = lane < n;
             if (valid) {
-                cpu = g_ld(sd + 64 + lane);
-                mem = g_ld(sd + 128 + lane);
-                req = g_ld(sd + 192 + lane);
-                conf = g_ld(sd + 256 + lane);
-                idx = g_ld(sd + 320 + lane);
+                idx = pos;
+                cpu = a.s_cpu[cb + pos];
+                mem = a.s_mem[cb + pos];
+                req = a.s_req[cb + pos];
+                conf = a.s_conf[cb + pos];
             }
             itail++;
         } else if (w == 0) {
@@ -748,9 +752,7 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
             if (fwd) {
                 uint32_t *sd = gout_data + (size_t)(ohead + (pos >= 64 ? 1 : 0)) * LSLOT;
-                const uint32_t p = pos & 63u;
-                g_st(sd + 64 + p, cpu); g_st(sd + 128 + p, mem); g_st(sd + 192 + p, req);
-                g_st(sd + 256 + p, conf); g_st(sd + 320 + p, idx);
+                g_st(sd + 64 + (pos & 63u), idx);
             }
             if (ofill + f >= 64) {
                 if (lane == 0) g_st(gout_data + (size_t)ohead * LSLOT, 64u);
@@ -1087,12 +1089,14 @@ bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint
     // placement frontier moves through them), so one wave does the same work in about the
     // same time while a scenario needs fewer registers than with 4-stage segments.
     const bool narrow = (uint64_t)S * NG <= kNarrowWaves;
-    // one-wave segments hold at most 20 groups: 20 groups take 158 VGPRs, three waves per
-    // SIMD (FP_WIDE_WAVES), 12 segments in flight per CU.  Config 4 (5k nodes, 79 groups):
-    // 4 segments of 20 groups 56.7 ms, 3 of 28 groups 58.2 ms at three waves per SIMD
-    // (spilling) / 68.7 ms at two, 5 of 16 groups 64.1 ms.
+    // one-wave segments hold at most 12 groups (<= 128 VGPRs, four waves per SIMD, 16
+    // segments in flight per CU).  With lagged segment tickets (the kernel) a segment runs
+    // on complete input, so more, smaller segments keep more waves busy: config 4 (79
+    // groups) 7 segments of 12 groups 28.3 ms, 10 of 8 groups 28.2, 4 of 20 groups 30.3,
+    // 3 of 24-28 groups 30.2.  (Without the lag, when a segment waited on its upstream
+    // half its life, 4 segments of 20 groups were best: 56.7 ms vs 64.1 for 5 of 16.)
     const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg
-                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : 20u;
+                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : 12u;
     const uint32_t B = (NG + seg_groups - 1) / seg_groups;
     const uint32_t per_seg = (NG + B - 1) / B;
     const uint32_t first_w = forced_w > 0 ? (uint32_t)forced_w : narrow ? 4u : 1u;
@@ -1121,7 +1125,7 @@ size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
     size_t lds;
     if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return 0;
     const size_t SC = (size_t)S * C, nlinks = (size_t)S * (B - 1), slots = (C + 63) / 64 + 2;
-    return 5 * SC * 4 + SC * 5 + 256 + nlinks * 128 + (size_t)S * B * 8 + 8 + nlinks * slots * 6 * 64 * 4 + 10 * 256;
+    return 5 * SC * 4 + SC * 5 + 256 + nlinks * 128 + (size_t)S * B * 8 + 8 + nlinks * slots * 2 * 64 * 4 + 10 * 256;
 }
 
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
@@ -1154,7 +1158,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     uint32_t *s_idx = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *ctl = (uint32_t *)fp_ws_take(c, 256 + nlinks * 128);  // ticket, abort | heads
     uint32_t *part = (uint32_t *)fp_ws_take(c, (size_t)S * B * 8 + 8);
-    uint32_t *gdata = nlinks ? (uint32_t *)fp_ws_take(c, nlinks * slots * 6 * 64 * 4) : nullptr;
+    uint32_t *gdata = nlinks ? (uint32_t *)fp_ws_take(c, nlinks * slots * 2 * 64 * 4) : nullptr;
     uint32_t *asg_s = (uint32_t *)fp_ws_take(c, SC * 4);  // plan in FFD order (k_unsort input)
     uint8_t *rsn_s = (uint8_t *)fp_ws_take(c, SC);
     if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx || !ctl || !part || (nlinks && !gdata) || !asg_s || !rsn_s)
