@@ -75,6 +75,7 @@ SIGNATURES = {
     "fp_dev_legacy_order": (ct.c_int, [vp, ct.POINTER(FpGraph), vp]),
     "fp_dev_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), vp, vp, vp]),
     "fp_dev_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),
+    "fp_place_ws_bytes": (ct.c_int, [vp, ct.c_uint32, ct.c_uint32, ct.c_uint32, u64p]),
     "fp_dev_feasibility": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), vp, vp, vp]),
     "fp_dev_feasibility_batch": (ct.c_int, [vp, ct.POINTER(FpBatch), vp, vp]),
     "fp_dev_argmin_cost": (ct.c_int, [vp, vp, ct.c_uint32, vp]),

@@ -208,6 +208,12 @@ extern "C" int fp_dev_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm)
     FP_HIP(hipSetDevice(c->device));
     return fp_dev_legacy_order_impl(c, g, perm);
 }
+extern "C" int fp_place_ws_bytes(fp_ctx *c, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes,
+                                 uint64_t *bytes_out) {
+    if (!c || !bytes_out) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_place_ws_bytes_impl(c, n_scen, n_containers, n_nodes, bytes_out);
+}
 extern "C" int fp_dev_feasibility_batch(fp_ctx *c, const fp_batch *b, uint32_t *first, uint32_t *count) {
     if (!c || !b) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));

@@ -76,7 +76,8 @@ int fp_dev_feasibility_batch_impl(fp_ctx *c, const fp_batch *b, uint32_t *first,
 
 // tile-pipeline FFD (fp_pipe.hip)
 bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out);
-size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N);
+size_t fp_pipe_ws_bytes(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N);
+int fp_place_ws_bytes_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint64_t *bytes);
 // bucket thresholds of the candidate masks: K ascending values, T[0] = 0
 constexpr int FP_BUCKETS = 32;
 void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T);  // geometric from lo to hi

@@ -75,10 +75,11 @@ struct PipeArgs {
     uint32_t B;       // segments (workgroups) per scenario
     uint32_t S;       // scenarios of the launch
     uint32_t lag;     // ticket lag between consecutive segments of a scenario (see the kernel)
-    uint32_t slots;   // slots per global link (every container fits: never blocks)
+    uint32_t slots;   // slots per global link: a ring when `bounded`, else every container fits
+    uint32_t bounded; // 1: links are rings with back-pressure (every segment co-resident, lag 0)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
-    uint32_t *ghead;  // [S][B-1] link heads, 128 B apart
+    uint32_t *ghead;  // [S][B-1] link control, 256 B apart: [0] head, [32] consumer tail
     uint32_t *gdata;  // [S][B-1][slots][2][64] link slots: row 0 = count, row 1 = FFD positions
     uint32_t *part;   // [S][B][2] per-segment (n_used, n_rej)
     const uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;  // FFD-sorted SoA [S][C]; idx bit31 = CYCLE
@@ -167,6 +168,37 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
     v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
     v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
+}
+
+constexpr size_t LCTL = 64;  // u32 per global link control block: [0] head, [LCTL / 2] tail
+
+// Bounded global link: wait (wave-uniform) until the producer may write every slot below
+// `need`, i.e. need - tail <= slots.  `seen` caches the consumer's tail so the common case
+// reads no memory.  Same abort and deadlock guard as the consumer's head poll.
+__device__ __forceinline__ bool gring_wait(uint32_t *tail, uint32_t need, uint32_t slots, uint32_t &seen,
+                                           const PipeArgs &a, uint32_t *abort_flag, uint32_t lane,
+                                           uint32_t &iters) {
+    if (need - seen <= slots) return true;
+    uint32_t n = 0;
+    uint64_t t0 = 0;
+    while (true) {
+        seen = __builtin_amdgcn_readfirstlane(g_ld(tail));
+        if (need - seen <= slots) { iters += n; return true; }
+        if (g_ld(a.gabort) || lds_acq(abort_flag)) return false;
+        if ((++n & 255u) == 0) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (!t0) {
+                t0 = now;
+            } else if (now - t0 > a.spin_ticks) {
+                g_st(a.gabort, 1u);
+                lds_rel(abort_flag, 1u);
+                if (lane == 0) atomicMax(a.err, (uint32_t)(-FP_EDEVICE));
+                return false;
+            }
+        }
+        if (n < 8) __builtin_amdgcn_s_sleep(2);
+        else __builtin_amdgcn_s_sleep(FP_SPIN_MAX);
+    }
 }
 
 // Node records (cpu_free, mem_free, conflict_used, labels) of a wave's tile live
@@ -387,10 +419,15 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
     // the consumer re-reads their fields from the sorted SoA (4 B per forwarded container
     // instead of 20: links sized for every container stay 5x smaller)
     const size_t LSLOT = 2 * 64;                        // u32 per global slot
-    uint32_t *gin_head = a.ghead + ((size_t)s * (B - 1) + (b - 1)) * 32;
+    uint32_t *gin_head = a.ghead + ((size_t)s * (B - 1) + (b - 1)) * LCTL;
     uint32_t *gin_data = a.gdata + ((size_t)s * (B - 1) + (b - 1)) * a.slots * LSLOT;
-    uint32_t *gout_head = a.ghead + ((size_t)s * (B - 1) + b) * 32;
+    uint32_t *gout_head = a.ghead + ((size_t)s * (B - 1) + b) * LCTL;
     uint32_t *gout_data = a.gdata + ((size_t)s * (B - 1) + b) * a.slots * LSLOT;
+    // bounded links: the consumer publishes how many slots it has finished with (tail, a
+    // separate 128-B line); the producer writes slot h only while h - tail < slots.  Slot
+    // index = sequence number mod slots (identity when unbounded: slots >= every slot).
+    const uint32_t gslots = a.slots, gbounded = a.bounded;
+    uint32_t otail_seen = 0;                            // last tail read from the consumer
     uint32_t *octl = CTL + w * 8;
     uint32_t *ictl = CTL + (w - 1) * 8;
     uint32_t *odata = D + (size_t)w * R * NF * 64;
@@ -436,7 +473,11 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             st_spin_in += n_sp;
             if (!got) break;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-            const uint32_t *sd = gin_data + (size_t)itail * LSLOT;
+            // slots before itail are finished with: their loads returned last iteration
+            // (the container fields they addressed were consumed), so the producer may
+            // reuse them.  Published every 4 slots (the ring keeps that much slack).
+            if (gbounded && (itail & 3u) == 0 && lane == 0) g_st(gin_head + LCTL / 2, itail);
+            const uint32_t *sd = gin_data + (size_t)(itail % gslots) * LSLOT;
             const uint32_t n = g_ld(sd);
             const uint32_t pos = g_ld(sd + 64 + lane);  // with the count: one round trip
             if (n & END) break;
@@ -750,12 +791,17 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             const uint32_t f = (uint32_t)__popcll(fm);
             if (!f) continue;
             const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+            // slots ohead and ohead + 1 must be free (wave-uniform; bounded links only)
+            if (gbounded && !gring_wait(gout_head + LCTL / 2, ohead + 2, gslots, otail_seen, a, abort_flag, lane, st_spin_out)) {
+                alive = false;
+                break;
+            }
             if (fwd) {
-                uint32_t *sd = gout_data + (size_t)(ohead + (pos >= 64 ? 1 : 0)) * LSLOT;
+                uint32_t *sd = gout_data + (size_t)((ohead + (pos >= 64 ? 1 : 0)) % gslots) * LSLOT;
                 g_st(sd + 64 + (pos & 63u), idx);
             }
             if (ofill + f >= 64) {
-                if (lane == 0) g_st(gout_data + (size_t)ohead * LSLOT, 64u);
+                if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, 64u);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 ohead++;
                 if (lane == 0) g_st(gout_head, ohead);
@@ -804,14 +850,15 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
     }
 
     // ---- flush + end of stream ----
-    if (g_out && !lds_acq(abort_flag)) {
+    if (g_out && !lds_acq(abort_flag) &&
+        (!gbounded || gring_wait(gout_head + LCTL / 2, ohead + 2, gslots, otail_seen, a, abort_flag, lane, st_spin_out))) {
         if (ofill) {
-            if (lane == 0) g_st(gout_data + (size_t)ohead * LSLOT, ofill);
+            if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, ofill);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ohead++;
             if (lane == 0) g_st(gout_head, ohead);
         }
-        if (lane == 0) g_st(gout_data + (size_t)ohead * LSLOT, END);
+        if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, END);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ohead++;
         if (lane == 0) g_st(gout_head, ohead);
@@ -1119,24 +1166,23 @@ bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint
     return false;
 }
 
-// Workspace bytes fp_pipe_launch takes (0 if the geometry does not fit).
-size_t fp_pipe_ws_bytes(uint32_t S, uint32_t C, uint32_t N) {
-    uint32_t G, W, B;
+// Launch geometry and link sizing for one fp_pipe_launch.
+struct PipeGeom {
+    uint32_t G, W, B, R;
     size_t lds;
-    if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return 0;
-    const size_t SC = (size_t)S * C, nlinks = (size_t)S * (B - 1), slots = (C + 63) / 64 + 2;
-    return 5 * SC * 4 + SC * 5 + 256 + nlinks * 128 + (size_t)S * B * 8 + 8 + nlinks * slots * 2 * 64 * 4 + 10 * 256;
-}
+    uint32_t lag;       // segment ticket lag (kernel comment)
+    uint32_t slots;     // slots per global link
+    uint32_t bounded;   // links are rings with back-pressure
+};
 
-int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
-                   const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
-                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
-                   const uint32_t *tm) {
-    uint32_t G, W, B;
-    size_t lds;
-    if (!fp_pipe_plan(S, N, &G, &W, &B, &lds)) return FP_EOVERFLOW;
-    if (C >= 0x80000000u) return FP_EOVERFLOW;
-    if ((uint64_t)S * B > 0xFFFFFFFFull) return FP_EOVERFLOW;
+// Global link ring size when every segment of the launch is co-resident: 256 slots x 64
+// containers in flight per link (128 KB).  FLEETPLACE_LINK_SLOTS overrides (>= 8; tests
+// force small rings to exercise back-pressure).
+constexpr uint32_t LINK_RING_SLOTS = 256;
+
+static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g) {
+    if (!fp_pipe_plan(S, N, &g->G, &g->W, &g->B, &g->lds)) return false;
+    const uint32_t G = g->G, W = g->W, B = g->B;
     // deepest ring (2..4 slots) that keeps two workgroups per CU (else one)
     uint32_t R = 2;
     for (uint32_t r = 4; r > 2; --r)
@@ -1146,24 +1192,83 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         const int fr = atoi(getenv("FLEETPLACE_PIPE_R"));
         if (fr >= 2 && fr <= 6 && lds_bytes(W, G, (uint32_t)fr) <= 160 * 1024) R = (uint32_t)fr;
     }
-    lds = lds_bytes(W, G, R);
+    g->R = R;
+    g->lds = lds_bytes(W, G, R);
+    // resident segments on this device (0 if unknown)
+    uint64_t slots_total = 0;
+    if (B > 1) {
+        int dev_cu = 0, occ = 0;
+        (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+        const bool wide = wide_g(W, G);
+        const void *fn = wide ? (G / 4 < sizeof(kKernelWide) / sizeof(kKernelWide[0]) ? kKernelWide[G / 4] : nullptr)
+                              : (G < sizeof(kKernel) / sizeof(kKernel[0]) ? kKernel[G] : nullptr);
+        if (fn && dev_cu > 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), g->lds) == hipSuccess && occ > 0)
+            slots_total = (uint64_t)occ * (uint64_t)dev_cu;
+    }
+    const bool fits = slots_total && (uint64_t)S * B <= slots_total;
+    // segment lag (kernel comment).  Measured FFD kernel ms (7 segments of 12 groups, 4096
+    // resident slots):
+    //   S=4096: lag 600 29.0, 1170 27.5, 2340 26.9, 3000 26.5, 4096 26.3
+    //   S=2048: lag 0 31.2, 256 19.2, 512 16.7, 1024 15.3, 2048 14.6
+    //   S=1024: lag 0 18.6, 256 12.2, 512 11.4, 1024 11.3
+    //   S=512 (fits at once): lag 0 10.8, 128 10.3, 512 10.6; S<=256 within 2%.
+    // A segment that never waits on its upstream beats overlap between a scenario's
+    // segments once the batch holds more segments than the GPU: lag = S runs the segments
+    // index by index (phase b starts as phase b-1's tickets drain).  Batches that fit at
+    // once keep lag 0 so all segments run concurrently.  FLEETPLACE_PIPE_LAG overrides.
+    g->lag = (B > 1 && S > 1 && slots_total && !fits) ? S : 0u;
+    if (getenv("FLEETPLACE_PIPE_LAG")) g->lag = (uint32_t)atoi(getenv("FLEETPLACE_PIPE_LAG"));
+    // Global links.  When every segment is resident at once and segments run side by side
+    // (lag 0), a link is a bounded ring: a producer waiting on a full ring waits on a
+    // consumer that is running, so back-pressure cannot deadlock.  Otherwise a consumer may
+    // start only after its producer finished (lag = S phases, or more segments than slots),
+    // so the link holds every container: (C + 63) / 64 + 2 slots.
+    const uint32_t full = (C + 63) / 64 + 2;
+    uint32_t ring = LINK_RING_SLOTS;
+    if (getenv("FLEETPLACE_LINK_SLOTS")) {
+        const int v = atoi(getenv("FLEETPLACE_LINK_SLOTS"));
+        if (v >= 8) ring = (uint32_t)v;
+    }
+    g->bounded = (fits && g->lag == 0 && ring < full) ? 1u : 0u;
+    g->slots = g->bounded ? ring : full;
+    return true;
+}
+
+// Workspace bytes fp_pipe_launch takes (0 if the geometry does not fit).
+size_t fp_pipe_ws_bytes(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N) {
+    PipeGeom g;
+    if (!pipe_geom(c, S, C, N, &g)) return 0;
+    const size_t SC = (size_t)S * C, nlinks = (size_t)S * (g.B - 1);
+    return 5 * SC * 4 + SC * 5 + 256 + nlinks * LCTL * 4 + (size_t)S * g.B * 8 + 8 + nlinks * g.slots * 2 * 64 * 4 +
+           10 * 256;
+}
+
+int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
+                   const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
+                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
+                   const uint32_t *tm) {
+    PipeGeom geo;
+    if (!pipe_geom(c, S, C, N, &geo)) return FP_EOVERFLOW;
+    const uint32_t G = geo.G, W = geo.W, B = geo.B, R = geo.R, slots = geo.slots;
+    const size_t lds = geo.lds;
+    if (C >= 0x80000000u) return FP_EOVERFLOW;
+    if ((uint64_t)S * B > 0xFFFFFFFFull) return FP_EOVERFLOW;
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;
-    const uint32_t slots = (C + 63) / 64 + 2;
     const size_t nlinks = (size_t)S * (B - 1);
     uint32_t *s_cpu = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_mem = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_req = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_conf = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *s_idx = (uint32_t *)fp_ws_take(c, SC * 4);
-    uint32_t *ctl = (uint32_t *)fp_ws_take(c, 256 + nlinks * 128);  // ticket, abort | heads
+    uint32_t *ctl = (uint32_t *)fp_ws_take(c, 256 + nlinks * LCTL * 4);  // ticket, abort | link control
     uint32_t *part = (uint32_t *)fp_ws_take(c, (size_t)S * B * 8 + 8);
     uint32_t *gdata = nlinks ? (uint32_t *)fp_ws_take(c, nlinks * slots * 2 * 64 * 4) : nullptr;
     uint32_t *asg_s = (uint32_t *)fp_ws_take(c, SC * 4);  // plan in FFD order (k_unsort input)
     uint8_t *rsn_s = (uint8_t *)fp_ws_take(c, SC);
     if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx || !ctl || !part || (nlinks && !gdata) || !asg_s || !rsn_s)
         return FP_ENOMEM;
-    FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * 128, st));
+    FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * LCTL * 4, st));
     {
         size_t g = (SC + 1023) / 1024;  // four elements per thread per pass
         if (g > 16384) g = 16384;
@@ -1180,25 +1285,10 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     }
     PipeArgs a;
     a.C = C; a.N = N; a.scen_base = scen_base; a.W = W; a.G = G; a.R = R;
-    a.B = B; a.slots = slots; a.ticket = ctl; a.gabort = ctl + 32; a.ghead = ctl + 64; a.gdata = gdata;
+    a.B = B; a.slots = slots; a.bounded = geo.bounded; a.ticket = ctl; a.gabort = ctl + 32; a.ghead = ctl + 64;
+    a.gdata = gdata;
     a.S = S;
-    // segment lag (kernel comment): twice the resident segments per segment index when
-    // there are enough scenarios, else 0.  FLEETPLACE_PIPE_LAG overrides (A/B, tests).
-    a.lag = 0;
-    if (B > 1 && S > 1) {
-        int dev_cu = 0, occ = 0;
-        (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
-        const bool wide = wide_g(W, G);
-        const void *fn = wide ? kKernelWide[G / 4] : kKernel[G];
-        if (fn && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), lds) == hipSuccess && occ > 0) {
-            const uint64_t slots_total = (uint64_t)occ * (uint64_t)(dev_cu > 0 ? dev_cu : 1);
-            // config 4 (3072 slots, 4 segments): lag 768 ran the FFD kernel in 31.7 ms, 1536 in
-            // 30.1, 256 in 37.1, 0 in 50.9
-            const uint64_t lag = 2 * slots_total / B;
-            a.lag = (uint32_t)(lag < S ? lag : S);
-        }
-    }
-    if (getenv("FLEETPLACE_PIPE_LAG")) a.lag = (uint32_t)atoi(getenv("FLEETPLACE_PIPE_LAG"));
+    a.lag = geo.lag;
     a.part = part;
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;

@@ -253,6 +253,46 @@ static inline unsigned grid_for(size_t n, unsigned block) {
     return (unsigned)(g ? g : 1);
 }
 
+// Workspace bytes fp_dev_place_batch takes for S scenarios of C containers x N nodes
+// (sort_tmp: the sorts' scratch share of it).
+static int place_ws_need(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, size_t *need, size_t *sort_tmp_out) {
+    hipStream_t st = c->stream;
+    const size_t SC = (size_t)S * C;
+    // device-wide sorts are sized for the widest key they may take (u64); the
+    // segmented fallback is used only when scenario + key bits exceed 64
+    size_t sort_tmp = 0, t = 0;
+    FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, SC, 0, 64, st));
+    sort_tmp = t;
+    FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, SC, 0, 32, st));
+    sort_tmp = t > sort_tmp ? t : sort_tmp;
+    FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                               (uint32_t *)nullptr, (uint32_t *)nullptr, (unsigned)SC, S,
+                                               (uint32_t *)nullptr, (uint32_t *)nullptr, 0, 32, st));
+    sort_tmp = t > sort_tmp ? t : sort_tmp;
+    FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, t, (uint64_t *)nullptr,
+                                               (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                               (uint32_t *)nullptr, (unsigned)SC, S,
+                                               (uint32_t *)nullptr, (uint32_t *)nullptr, 0, 64, st));
+    sort_tmp = t > sort_tmp ? t : sort_tmp;
+    const size_t pipe_ws = fp_pipe_ws_bytes(c, S, C, N);
+    if (pipe_ws == 0) return FP_EOVERFLOW;
+    const size_t rank_ws = 2 * (2 * RANK_WORDS * 4 + RANK_MAX_VALUE * 4) + 2 * 256;
+    *need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + pipe_ws + rank_ws + 16 * 256;
+    *sort_tmp_out = sort_tmp;
+    return FP_OK;
+}
+
+int fp_place_ws_bytes_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint64_t *bytes) {
+    if (S == 0 || C == 0) { *bytes = 0; return FP_OK; }
+    if ((size_t)S * C > 0xFFFFFFFFull) return FP_EOVERFLOW;
+    size_t need = 0, sort_tmp = 0;
+    if (int rc = place_ws_need(c, S, C, N, &need, &sort_tmp)) return rc;
+    *bytes = need;
+    return FP_OK;
+}
+
 int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     const uint32_t S = b->n_scen, C = b->n_containers, N = b->n_nodes;
     if (S == 0) return FP_OK;
@@ -275,28 +315,8 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         return FP_EINVAL;
 
     // ---- workspace ----
-    // device-wide sorts are sized for the widest key they may take (u64); the
-    // segmented fallback is used only when scenario + key bits exceed 64
-    size_t sort_tmp = 0, t = 0;
-    FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
-                                     (uint32_t *)nullptr, SC, 0, 64, st));
-    sort_tmp = t;
-    FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                     (uint32_t *)nullptr, SC, 0, 32, st));
-    sort_tmp = t > sort_tmp ? t : sort_tmp;
-    FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                               (uint32_t *)nullptr, (uint32_t *)nullptr, (unsigned)SC, S,
-                                               (uint32_t *)nullptr, (uint32_t *)nullptr, 0, 32, st));
-    sort_tmp = t > sort_tmp ? t : sort_tmp;
-    FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, t, (uint64_t *)nullptr,
-                                               (uint64_t *)nullptr, (uint32_t *)nullptr,
-                                               (uint32_t *)nullptr, (unsigned)SC, S,
-                                               (uint32_t *)nullptr, (uint32_t *)nullptr, 0, 64, st));
-    sort_tmp = t > sort_tmp ? t : sort_tmp;
-    const size_t pipe_ws = fp_pipe_ws_bytes(S, C, N);
-    if (pipe_ws == 0) return FP_EOVERFLOW;
-    const size_t rank_ws = 2 * (2 * RANK_WORDS * 4 + RANK_MAX_VALUE * 4) + 2 * 256;
-    const size_t need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + pipe_ws + rank_ws + 16 * 256;
+    size_t need = 0, sort_tmp = 0;
+    if (int rc0 = place_ws_need(c, S, C, N, &need, &sort_tmp)) return rc0;
     int rc = fp_ws_reserve(c, need);
     if (rc) return rc;
     fp_ws_reset(c);

@@ -167,6 +167,12 @@ class Planner:
                                          count_t.data_ptr(), bitmap_t.data_ptr() if bitmap_t is not None else None),
               "fp_dev_feasibility")
 
+    def place_ws_bytes(self, S: int, C: int, N: int) -> int:
+        """Device workspace bytes a place batch of S x C x N takes on this context."""
+        out = ct.c_uint64(0)
+        check(self._L.fp_place_ws_bytes(self._ctx, S, C, N, ct.byref(out)), "fp_place_ws_bytes")
+        return int(out.value)
+
     def dev_feasibility_batch(self, db: "DevBatch", first_t, count_t):
         """Stage 2 over every scenario of ``db`` ([S*C] outputs, scenario-major)."""
         check(self._L.fp_dev_feasibility_batch(self._ctx, ct.byref(db.struct()), first_t.data_ptr(),

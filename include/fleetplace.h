@@ -145,6 +145,12 @@ int fp_dev_legacy_order(fp_ctx *ctx, const fp_graph *g, uint32_t *perm_out);
 int fp_dev_levelize(fp_ctx *ctx, const fp_graph *g, uint32_t *level_out, uint32_t *order_out,
                     uint32_t *n_cycle_out_dev);
 int fp_dev_place_batch(fp_ctx *ctx, const fp_batch *b);
+/* Device workspace (bytes) fp_place_batch / fp_dev_place_batch take on this ctx for
+ * n_scen scenarios of n_containers x n_nodes (0 when there is nothing to place); the ctx
+ * grows its workspace to it on the first such call and keeps it.  Depends on the device
+ * (the pipeline's link sizing follows its occupancy). */
+int fp_place_ws_bytes(fp_ctx *ctx, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes,
+                      uint64_t *bytes_out);
 int fp_dev_feasibility(fp_ctx *ctx, const fp_containers *c, const fp_nodes *nodes,
                        uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out);
 /* Stage 2 batched over what-if scenarios: for each scenario s and container c of b

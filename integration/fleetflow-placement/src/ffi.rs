@@ -105,6 +105,8 @@ unsafe extern "C" {
     pub fn fp_dev_levelize(ctx: *mut fp_ctx, g: *const fp_graph, level_out: *mut u32, order_out: *mut u32,
                            n_cycle_out_dev: *mut u32) -> c_int;
     pub fn fp_dev_place_batch(ctx: *mut fp_ctx, b: *const fp_batch) -> c_int;
+    pub fn fp_place_ws_bytes(ctx: *mut fp_ctx, n_scen: u32, n_containers: u32, n_nodes: u32,
+                             bytes_out: *mut u64) -> c_int;
     pub fn fp_dev_feasibility(ctx: *mut fp_ctx, c: *const fp_containers, nodes: *const fp_nodes,
                               first_out: *mut u32, count_out: *mut u32, bitmap_out: *mut u64) -> c_int;
     pub fn fp_dev_feasibility_batch(ctx: *mut fp_ctx, b: *const fp_batch, first_out: *mut u32,

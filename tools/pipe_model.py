@@ -82,6 +82,8 @@ def main():
                                                   "note": "C++ loop diagnostics build only (FP_NO_ASM)"},
                     "per_stage": [{"visits": r[0] / S, "checks": r[1] / S, "hits": r[2] / S,
                                    "cand_Mcycles": r[10] / S / 1e6, "prescan_Mcycles": r[9] / S / 1e6,
+                                   "input_Mcycles": r[8] / S / 1e6, "spin_in_per_batch": r[4] / max(r[3], 1),
+                                   "fwd_Mcycles": r[11] / S / 1e6, "batches": r[3] / S,
                                    "life_Mcycles": r[13] / S / 1e6} for r in v]}
         print(leg, json.dumps(res[leg]), flush=True)
     with open(out_path, "w") as fo:

@@ -7,11 +7,11 @@ root=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$root/gpurun_out/sq_$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
-args="$root/bench.py --no-cpu-baseline --steps 2 --warmup 1"
+args="$root/bench.py --no-cpu-baseline --no-config3 --no-stage2 --steps 2 --warmup 1"
 i=0
 for pmc in "SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "SQ_WAIT_ANY SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_INSTS SQ_IFETCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
-           "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ SQC_ICACHE_MISSES_DUPLICATE"; do
+           "SQ_INSTS_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d "$out/p$i" -o run -- python3 $args > "$out/p$i.log" 2>&1
 done
