@@ -48,6 +48,11 @@ __device__ unsigned long long g_pipe_stats[16 * 16];
 // per-batch timeline of scenario 0: [stage][batch] = (t_in_ready, t_prescan, t_cand, t_out_done)
 constexpr int TL_B = 2048;
 __device__ unsigned long long g_pipe_tl[16 * TL_B * 8];
+// per global stage of scenario 0 (s_memrealtime, 100 MHz, device-wide): [0] start [1] first
+// input [2] loop end [3] busy cycles (prescan + candidate loop, s_memtime) [4] batches
+// [5] output-wait cycles [6] input-spin iterations [7] placements
+constexpr int SPAN_MAX = 4096;
+__device__ unsigned long long g_stage_span[SPAN_MAX * 8];
 #else
 #define STAT_ADD(w, i, v) ((void)0)
 #define STAT_CLK() 0ull
@@ -77,6 +82,7 @@ struct PipeArgs {
     uint32_t lag;     // ticket lag between consecutive segments of a scenario (see the kernel)
     uint32_t slots;   // slots per global link: a ring when `bounded`, else every container fits
     uint32_t bounded; // 1: links are rings with back-pressure (every segment co-resident, lag 0)
+    uint32_t flush;   // idle flushes of partial output slots: bit 0 LDS rings, bit 1 global links (bounded)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
     uint32_t *ghead;  // [S][B-1] link control, 256 B apart: [0] head, [32] consumer tail
@@ -237,6 +243,13 @@ using RecT = uint32_t[G];
 #ifndef FP_PF_MAX
 #define FP_PF_MAX 16
 #endif
+// the serial loop over one group's queue: the exec-masked loop (fp_pipe_asm.h,
+// fpp_group_x: 172 vs 264 cycles per container in tools/ubench/place.hip); -DFP_GROUP_LOOP=
+// fpp_asm_group selects round 2's readlane / writelane loop for A/B runs
+#ifndef FP_GROUP_LOOP
+#define FP_GROUP_LOOP fpp_group_x
+#endif
+#define FPP_GROUP_LOOP FP_GROUP_LOOP
 template <uint32_t G, bool UPD, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
@@ -271,7 +284,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
             }
             if (q) {
                 uint64_t touched = 0;
-                fpp_asm_group<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                FPP_GROUP_LOOP<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                      req, conf, cand, cand_hi, gb64, nchk, nhit);
                 if (touched) {
                     const bool me = (touched >> lane) & 1ull;
@@ -443,6 +456,10 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
     unsigned long long ck_in = 0, ck_pre = 0, ck_cand = 0, ck_fwd = 0, ck_wait = 0;
     const unsigned long long ck_t0 = STAT_CLK();
     unsigned long long ck_a, ck_b;
+#ifdef FP_PIPE_STATS
+    const unsigned long long sp_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long sp_first = 0;
+#endif
     bool alive = true;
     while (alive) {
         ck_a = STAT_CLK();
@@ -476,7 +493,9 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             // slots before itail are finished with: their loads returned last iteration
             // (the container fields they addressed were consumed), so the producer may
             // reuse them.  Published every 4 slots (the ring keeps that much slack).
-            if (gbounded && (itail & 3u) == 0 && lane == 0) g_st(gin_head + LCTL / 2, itail);
+            // With idle flushes the producer reads it as "the consumer is on my last slot":
+            // published every slot then.
+            if (((a.flush & 2u) || (gbounded && (itail & 3u) == 0)) && lane == 0) g_st(gin_head + LCTL / 2, itail);
             const uint32_t *sd = gin_data + (size_t)(itail % gslots) * LSLOT;
             const uint32_t n = g_ld(sd);
             const uint32_t pos = g_ld(sd + 64 + lane);  // with the count: one round trip
@@ -528,8 +547,16 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             itail++;
             lds_rel(&ictl[1], itail);
         }
+        // idle flush (global link): the consumer's tail, loaded now and used after the
+        // candidate loop, so its round trip overlaps this batch's work
+        uint32_t tail_async = 0;
+        const bool tail_issued = (a.flush & 2u) && g_out && ofill != 0;
+        if (tail_issued) tail_async = g_ld(gout_head + LCTL / 2);
         const uint32_t kc = bucket_of(cpu, my_t, 0), km = bucket_of(mem, my_t, K);
         ck_b = STAT_CLK(); ck_in += ck_b - ck_a; ck_a = ck_b;
+#ifdef FP_PIPE_STATS
+        if (!sp_first) sp_first = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef FP_PIPE_STATS
         const unsigned long long ck_t0_batch = ck_b;
 #endif
@@ -785,29 +812,43 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         }
 #endif
         const bool fwd = valid && !((placed >> lane) & 1ull);
+        // Idle flush: a partial output slot normally waits until 64 containers fill it.  While
+        // the consumer is idle (it has taken every published slot) that wait is pure latency
+        // on the FFD chain -- the first containers a filling stage rejects are exactly what the
+        // next stage needs to start its own fill -- so the partial slot is published at once.
         if (g_out) {
             // append to the open global slot; publish each full slot (never blocks)
             const uint64_t fm = __builtin_amdgcn_ballot_w64(fwd);
             const uint32_t f = (uint32_t)__popcll(fm);
-            if (!f) continue;
-            const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-            // slots ohead and ohead + 1 must be free (wave-uniform; bounded links only)
-            if (gbounded && !gring_wait(gout_head + LCTL / 2, ohead + 2, gslots, otail_seen, a, abort_flag, lane, st_spin_out)) {
-                alive = false;
-                break;
+            if (f) {
+                const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+                // slots ohead and ohead + 1 must be free (wave-uniform; bounded links only)
+                if (gbounded &&
+                    !gring_wait(gout_head + LCTL / 2, ohead + 2, gslots, otail_seen, a, abort_flag, lane, st_spin_out)) {
+                    alive = false;
+                    break;
+                }
+                if (fwd) {
+                    uint32_t *sd = gout_data + (size_t)((ohead + (pos >= 64 ? 1 : 0)) % gslots) * LSLOT;
+                    g_st(sd + 64 + (pos & 63u), idx);
+                }
+                if (ofill + f >= 64) {
+                    if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, 64u);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    ohead++;
+                    if (lane == 0) g_st(gout_head, ohead);
+                    ofill = ofill + f - 64;
+                } else {
+                    ofill += f;
+                }
             }
-            if (fwd) {
-                uint32_t *sd = gout_data + (size_t)((ohead + (pos >= 64 ? 1 : 0)) % gslots) * LSLOT;
-                g_st(sd + 64 + (pos & 63u), idx);
-            }
-            if (ofill + f >= 64) {
-                if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, 64u);
+            // the consumer publishes slot j's index when it takes slot j (tail lags by one)
+            if (tail_issued && ofill && __builtin_amdgcn_readfirstlane(tail_async) + 1u >= ohead) {
+                if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, ofill);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 ohead++;
                 if (lane == 0) g_st(gout_head, ohead);
-                ofill = ofill + f - 64;
-            } else {
-                ofill += f;
+                ofill = 0;
             }
             continue;
         }
@@ -821,34 +862,54 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         }
         const uint64_t fm = __ballot(fwd);
         const uint32_t f = (uint32_t)__popcll(fm);
-        if (!f) continue;
-        const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-        uint32_t *od = odata + (size_t)(ohead % R) * NF * 64;
-        if (fwd && pos < 64) {
-            od[pos] = cpu; od[64 + pos] = mem; od[128 + pos] = req; od[192 + pos] = conf; od[256 + pos] = idx;
+        if (f) {
+            const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+            uint32_t *od = odata + (size_t)(ohead % R) * NF * 64;
+            if (fwd && pos < 64) {
+                od[pos] = cpu; od[64 + pos] = mem; od[128 + pos] = req; od[192 + pos] = conf; od[256 + pos] = idx;
+            }
+            if (ofill + f >= 64) {
+                octl[2 + ohead % R] = 64;
+                ohead++;
+                lds_rel(&octl[0], ohead);
+                const uint32_t h = ohead;
+                ck_b = STAT_CLK(); ck_fwd += ck_b - ck_a; ck_a = ck_b;
+                if (!spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, a.spin_ticks, st_spin_out)) {
+                    alive = false;
+                    break;
+                }
+                ck_b = STAT_CLK(); ck_wait += ck_b - ck_a; ck_a = ck_b;
+                od = odata + (size_t)(ohead % R) * NF * 64;
+                if (fwd && pos >= 64) {
+                    const uint32_t p = pos - 64;
+                    od[p] = cpu; od[64 + p] = mem; od[128 + p] = req; od[192 + p] = conf; od[256 + p] = idx;
+                }
+                ofill = ofill + f - 64;
+            } else {
+                ofill += f;
+            }
         }
-        if (ofill + f >= 64) {
-            octl[2 + ohead % R] = 64;
+        // idle flush (see the global link above): the consumer has taken every published slot
+        if ((a.flush & 1u) && ofill && lds_acq(&octl[1]) == ohead) {
+            octl[2 + ohead % R] = ofill;
             ohead++;
             lds_rel(&octl[0], ohead);
             const uint32_t h = ohead;
-            ck_b = STAT_CLK(); ck_fwd += ck_b - ck_a; ck_a = ck_b;
             if (!spin(&octl[1], [h, R](uint32_t tl) { return h - tl < R; }, abort_flag, a.err, a.spin_ticks, st_spin_out)) {
                 alive = false;
                 break;
             }
-            ck_b = STAT_CLK(); ck_wait += ck_b - ck_a; ck_a = ck_b;
-            od = odata + (size_t)(ohead % R) * NF * 64;
-            if (fwd && pos >= 64) {
-                const uint32_t p = pos - 64;
-                od[p] = cpu; od[64 + p] = mem; od[128 + p] = req; od[192 + p] = conf; od[256 + p] = idx;
-            }
-            ofill = ofill + f - 64;
-        } else {
-            ofill += f;
+            ofill = 0;
         }
     }
 
+#ifdef FP_PIPE_STATS
+    if (s == 0 && lane == 0 && b * W + w < (uint32_t)SPAN_MAX) {
+        unsigned long long *sp = &g_stage_span[(size_t)(b * W + w) * 8];
+        sp[0] = sp_start; sp[1] = sp_first; sp[2] = __builtin_amdgcn_s_memrealtime();
+        sp[3] = ck_pre + ck_cand; sp[4] = st_batches; sp[5] = ck_wait; sp[6] = st_spin_in; sp[7] = st_hits;
+    }
+#endif
     // ---- flush + end of stream ----
     if (g_out && !lds_acq(abort_flag) &&
         (!gbounded || gring_wait(gout_head + LCTL / 2, ohead + 2, gslots, otail_seen, a, abort_flag, lane, st_spin_out))) {
@@ -1289,6 +1350,12 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.gdata = gdata;
     a.S = S;
     a.lag = geo.lag;
+    // idle flushes: LDS rings always (producer and consumer share the workgroup); global links
+    // only when bounded -- their consumer runs beside the producer and back-pressure bounds
+    // the extra partial slots (an unbounded link is sized for full slots only).
+    // FLEETPLACE_PIPE_FLUSH = mask of the two (0 disables).
+    a.flush = geo.bounded ? 3u : 1u;
+    if (getenv("FLEETPLACE_PIPE_FLUSH")) a.flush &= (uint32_t)atoi(getenv("FLEETPLACE_PIPE_FLUSH"));
     a.part = part;
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
@@ -1330,6 +1397,11 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
 #ifdef FP_PIPE_STATS
 extern "C" int fp_debug_pipe_timeline(unsigned long long *out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_tl), sizeof(unsigned long long) * 16 * TL_B * 8) != hipSuccess)
+        return FP_EDEVICE;
+    return FP_OK;
+}
+extern "C" int fp_debug_stage_span(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_span), sizeof(unsigned long long) * SPAN_MAX * 8) != hipSuccess)
         return FP_EDEVICE;
     return FP_OK;
 }

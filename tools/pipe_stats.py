@@ -78,7 +78,24 @@ def timeline(out_path):
                     fo.write(f"{w},{b}," + ",".join(str(x) for x in v) + "\n")
 
 
+def stage_span(out_path):
+    """Dump scenario 0's per-stage span (stats build) to out_path as CSV: realtime ticks (100 MHz)."""
+    L = _lib.load()
+    f = L.fp_debug_stage_span
+    f.argtypes = [ct.POINTER(ct.c_ulonglong)]
+    buf = (ct.c_ulonglong * (4096 * 8))()
+    f(buf)
+    with open(out_path, "w") as fo:
+        fo.write("stage,start,first,end,busy_cyc,batches,wait_cyc,spin_in,hits\n")
+        for w in range(4096):
+            v = [buf[w * 8 + i] for i in range(8)]
+            if v[0]:
+                fo.write(f"{w}," + ",".join(str(x) for x in v) + "\n")
+
+
 if __name__ == "__main__":
     main()
     if os.environ.get("TIMELINE"):
         timeline(os.environ["TIMELINE"])
+    if os.environ.get("SPAN"):
+        stage_span(os.environ["SPAN"])
