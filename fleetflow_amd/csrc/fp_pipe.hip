@@ -74,6 +74,7 @@ constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per grou
 #define FP_SPIN_MAX 12              // longest back-off sleep of an idle stage (x 64 cycles)
 #endif
 constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
+constexpr uint32_t IDX_POS_MASK = (1u << 21) - 1;  // position bits of a packed s_idx word
 
 struct PipeArgs {
     uint32_t C, N, scen_base, W, G, R;
@@ -83,6 +84,7 @@ struct PipeArgs {
     uint32_t slots;   // slots per global link: a ring when `bounded`, else every container fits
     uint32_t bounded; // 1: links are rings with back-pressure (every segment co-resident, lag 0)
     uint32_t flush;   // idle flushes of partial output slots: bit 0 LDS rings, bit 1 global links (bounded)
+    uint32_t kpack;   // 1: s_idx carries the bucket indices (bits 21-25 cpu, 26-30 mem; C <= 2^21)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
     uint32_t *ghead;  // [S][B-1] link control, 256 B apart: [0] head, [32] consumer tail
@@ -326,6 +328,8 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t C = a.C, N = a.N;
+    // the FFD position inside an s_idx word (above it: CYCLE bit 31, packed buckets)
+    const uint32_t pmask = a.kpack ? IDX_POS_MASK : ~CYC;
     // per-lane group bit sets (schedulable / candidate groups): 64-bit above 32 groups
     using GM = typename std::conditional<(G > 32), uint64_t, uint32_t>::type;
 
@@ -502,11 +506,12 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             if (n & END) break;
             valid = lane < n;
             if (valid) {
-                idx = pos;
-                cpu = a.s_cpu[cb + pos];
-                mem = a.s_mem[cb + pos];
-                req = a.s_req[cb + pos];
-                conf = a.s_conf[cb + pos];
+                idx = pos;  // the packed s_idx word (position | buckets)
+                const uint32_t p = pos & pmask;
+                cpu = a.s_cpu[cb + p];
+                mem = a.s_mem[cb + p];
+                req = a.s_req[cb + p];
+                conf = a.s_conf[cb + p];
             }
             itail++;
         } else if (w == 0) {
@@ -522,7 +527,7 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             }
             const bool cyc = valid && (idx & CYC);
             if (cyc) {
-                const uint32_t j = idx & ~CYC;
+                const uint32_t j = idx & pmask;
                 a.assign[cb + j] = FP_NONE;
                 a.reason[cb + j] = FP_REASON_CYCLE;
             }
@@ -552,7 +557,16 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         uint32_t tail_async = 0;
         const bool tail_issued = (a.flush & 2u) && g_out && ofill != 0;
         if (tail_issued) tail_async = g_ld(gout_head + LCTL / 2);
-        const uint32_t kc = bucket_of(cpu, my_t, 0), km = bucket_of(mem, my_t, K);
+        // bucket indices: packed into s_idx by k_gather_sorted (one binary search per container
+        // instead of one per container and stage), else searched here
+        uint32_t kc, km;
+        if (a.kpack) {
+            kc = (idx >> 21) & (uint32_t)(K - 1);
+            km = (idx >> 26) & (uint32_t)(K - 1);
+        } else {
+            kc = bucket_of(cpu, my_t, 0);
+            km = bucket_of(mem, my_t, K);
+        }
         ck_b = STAT_CLK(); ck_in += ck_b - ck_a; ck_a = ck_b;
 #ifdef FP_PIPE_STATS
         if (!sp_first) sp_first = __builtin_amdgcn_s_memrealtime();
@@ -571,7 +585,11 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         //    cpu.  One corner per 64-container batch ran the config-4 bench 12% faster
         //    than one per 8 containers (1.64 vs 1.96 checks per container, but an 8x
         //    cheaper prescan on every stage a container visits).
-        const uint32_t qc = wave_min(valid ? cpu : 0xFFFFFFFFu), qm = wave_min(valid ? mem : 0xFFFFFFFFu);
+        // the valid lanes are a prefix holding the batch in FFD order (cpu non-increasing), so the
+        // smallest cpu is the last valid lane's
+        const uint64_t vm = __builtin_amdgcn_ballot_w64(valid);
+        const uint32_t qc = vm ? __builtin_amdgcn_readlane(cpu, 63 - __builtin_clzll(vm)) : 0xFFFFFFFFu;
+        const uint32_t qm = wave_min(valid ? mem : 0xFFFFFFFFu);
         // every mask load is issued before the first use (no per-group LDS round trip)
         const uint32_t oc = kc * 2, om = km * 2 + 1;
         GM cand = 0;
@@ -800,8 +818,8 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         const uint32_t tl_idx = st_batches - 1;
 #endif
         if ((placed >> lane) & 1ull) {
-            a.assign[cb + idx] = my_assign;
-            a.reason[cb + idx] = FP_REASON_OK;
+            a.assign[cb + (idx & pmask)] = my_assign;
+            a.reason[cb + (idx & pmask)] = FP_REASON_OK;
         }
 #ifdef FP_PIPE_STATS
         if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B && b * W + w < 16) {
@@ -854,8 +872,8 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
         }
         if (!has_out) {
             if (fwd) {
-                a.assign[cb + idx] = FP_NONE;
-                a.reason[cb + idx] = FP_REASON_NOFIT;
+                a.assign[cb + (idx & pmask)] = FP_NONE;
+                a.reason[cb + (idx & pmask)] = FP_REASON_NOFIT;
             }
             n_rej += (uint32_t)__popcll(__ballot(fwd));
             continue;
@@ -998,8 +1016,14 @@ __global__ void k_cost_reduce(uint32_t S, uint32_t B, uint32_t scen_base, const 
 // (b % 8) * (grid / 8) + b / 8 gives each XCD a contiguous eighth of every grid-stride
 // pass -- about ten config-4 scenarios, whose random req/conf reads then stay in that
 // XCD's 4 MB L2 instead of being fetched by all eight.
+// bucket thresholds for k_gather_sorted (by value: [0, K) cpu, [K, 2K) mem)
+struct GatherThr {
+    uint32_t t[2 * K];
+    uint32_t kpack;
+};
+
 template <class KeyT>
-__global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
+__global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
                                 const KeyT *__restrict__ skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax,
                                 const uint32_t *__restrict__ cval, const uint32_t *__restrict__ mval,
                                 const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
@@ -1011,6 +1035,16 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
     // independent elements per thread in flight (the req/conf gathers are dependent loads)
     const uint32_t total = S * C, stride = gridDim.x * blockDim.x;
     const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    __shared__ uint32_t T[2 * K];
+    if (threadIdx.x < 2 * K) T[threadIdx.x] = th.t[threadIdx.x];
+    __syncthreads();
+    // largest k with T[k] <= v (T ascending, T[0] = 0)
+    auto bucket = [](const uint32_t *t, uint32_t v) {
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = K / 2; step; step >>= 1) k += t[k + step] <= v ? step : 0u;
+        return k;
+    };
     for (size_t i0 = (size_t)lb * blockDim.x + threadIdx.x; i0 < total; i0 += 4 * (size_t)stride) {
         uint32_t j[4], src[4], r[4], f[4], cy[4], cv[4], mv[4], pos[4];
 #pragma unroll
@@ -1058,7 +1092,8 @@ __global__ void k_gather_sorted(uint32_t S, uint32_t C, const uint32_t *__restri
                 __builtin_nontemporal_store(f[u], &s_conf[i]);
                 // the pipeline carries the SORTED position: its assign/reason stores land
                 // next to each other (k_unsort restores container order, coalesced)
-                __builtin_nontemporal_store(pos[u] | cy[u], &s_idx[i]);
+                const uint32_t kb = th.kpack ? (bucket(T, cv[u]) << 21) | (bucket(T + K, mv[u]) << 26) : 0u;
+                __builtin_nontemporal_store(pos[u] | kb | cy[u], &s_idx[i]);
             }
         }
     }
@@ -1330,17 +1365,23 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx || !ctl || !part || (nlinks && !gdata) || !asg_s || !rsn_s)
         return FP_ENOMEM;
     FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * LCTL * 4, st));
+    // buckets ride in s_idx when positions fit 21 bits (FLEETPLACE_NO_KPACK=1: search per stage)
+    const uint32_t kpack = C <= (IDX_POS_MASK + 1u) && !(getenv("FLEETPLACE_NO_KPACK") && atoi(getenv("FLEETPLACE_NO_KPACK")));
+    GatherThr gth;
+    memcpy(gth.t, tc, sizeof(uint32_t) * K);
+    memcpy(gth.t + K, tm, sizeof(uint32_t) * K);
+    gth.kpack = kpack;
     {
         size_t g = (SC + 1023) / 1024;  // four elements per thread per pass
         if (g > 16384) g = 16384;
         if (g >= 64) g = (g + 7) & ~(size_t)7;  // a multiple of 8: XCD-contiguous mapping
         if (key_bytes == 4)
             k_gather_sorted<uint32_t><<<(unsigned)g, 256, 0, st>>>(
-                S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
+                gth, S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
                 b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
         else
             k_gather_sorted<uint64_t><<<(unsigned)g, 256, 0, st>>>(
-                S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
+                gth, S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
                 b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
         FP_HIP(hipGetLastError());
     }
@@ -1350,6 +1391,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.gdata = gdata;
     a.S = S;
     a.lag = geo.lag;
+    a.kpack = kpack;
     // idle flushes: LDS rings always (producer and consumer share the workgroup); global links
     // only when bounded -- their consumer runs beside the producer and back-pressure bounds
     // the extra partial slots (an unbounded link is sized for full slots only).

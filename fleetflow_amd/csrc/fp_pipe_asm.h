@@ -319,187 +319,4 @@ __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64
     }
 }
 
-// Variant of fpp_asm_group_x: the feasibility tests are v_cmpx (exec &= test), so the
-// feasible set lands in exec with no VALU -> SALU mask round trip; two containers per
-// iteration with the next container's readlanes issued ahead (software pipelined).
-__device__ __forceinline__ void fpp_asm_group_y(uint64_t q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
-                                                uint32_t &rmf, uint32_t &rcu, uint32_t rlab, uint32_t cpu,
-                                                uint32_t mem, uint32_t req, uint32_t conf, uint32_t gbg,
-                                                uint32_t &nchk) {
-    uint32_t ta, tb, ac, am, ar, ax, bc, bm, br, bx, l, nv;
-    uint64_t m2, esv;
-    uint32_t t0;
-#define FGY_ONE(T, KC, KM, KR, KX, TN, NC, NM, NR, NX)                                     \
-        "v_cmpx_le_u32_e32 %[" KC "], %[rcf]\n\t"                                        \
-        "v_cmpx_le_u32_e32 %[" KM "], %[rmf]\n\t"                                        \
-        "v_and_b32_e32 %[t0], %[" KR "], %[rlab]\n\t"                                    \
-        "v_and_or_b32 %[t0], %[rcu], %[" KX "], %[t0]\n\t"                               \
-        "v_cmpx_eq_u32_e32 0, %[t0]\n\t"                                                 \
-        "s_ff1_i32_b64 %[" TN "], %[q]\n\t"                                              \
-        "s_bitset0_b64 %[q], %[" TN "]\n\t"                                              \
-        "s_ff1_i32_b64 %[l], exec\n\t"                                                   \
-        "s_lshl_b64 %[m2], 1, %[l]\n\t"                                                  \
-        "s_and_b64 exec, exec, %[m2]\n\t"                                                \
-        "v_subrev_u32_e32 %[rcf], %[" KC "], %[rcf]\n\t"                                 \
-        "v_subrev_u32_e32 %[rmf], %[" KM "], %[rmf]\n\t"                                 \
-        "v_or_b32_e32 %[rcu], %[" KX "], %[rcu]\n\t"                                     \
-        "s_or_b64 %[touched], %[touched], exec\n\t"                                      \
-        "s_or_b32 %[nv], %[gbg], %[l]\n\t"                                               \
-        "s_lshl_b64 exec, 1, %[" T "]\n\t"                                               \
-        "v_mov_b32_e32 %[asg], %[nv]\n\t"                                                \
-        "s_mov_b64 exec, %[esv]\n\t"                                                     \
-        "v_readlane_b32 %[" NC "], %[cpu], %[" TN "]\n\t"                                \
-        "v_readlane_b32 %[" NM "], %[mem], %[" TN "]\n\t"                                \
-        "v_readlane_b32 %[" NR "], %[req], %[" TN "]\n\t"                                \
-        "v_readlane_b32 %[" NX "], %[conf], %[" TN "]\n\t"
-    asm volatile(
-        "s_cmp_eq_u64 %[q], 0\n\t"
-        "s_cbranch_scc1 .Lfgy_end%=\n\t"
-        "s_mov_b64 %[esv], exec\n\t"
-        "s_ff1_i32_b64 %[ta], %[q]\n\t"
-        "s_bitset0_b64 %[q], %[ta]\n\t"
-        "v_readlane_b32 %[ac], %[cpu], %[ta]\n\t"
-        "v_readlane_b32 %[am], %[mem], %[ta]\n\t"
-        "v_readlane_b32 %[ar], %[req], %[ta]\n\t"
-        "v_readlane_b32 %[ax], %[conf], %[ta]\n\t"
-        "s_nop 1\n"
-        ".Lfgy_loop%=:\n\t"
-        FGY_ONE("ta", "ac", "am", "ar", "ax", "tb", "bc", "bm", "br", "bx")
-        "s_cmp_lt_i32 %[tb], 0\n\t"
-        "s_cbranch_scc1 .Lfgy_done%=\n\t"
-        FGY_ONE("tb", "bc", "bm", "br", "bx", "ta", "ac", "am", "ar", "ax")
-        "s_cmp_lt_i32 %[ta], 0\n\t"
-        "s_cbranch_scc0 .Lfgy_loop%=\n"
-        ".Lfgy_done%=:\n\t"
-        "s_mov_b64 exec, %[esv]\n"
-        ".Lfgy_end%=:"
-        : [q] "+s"(q), [touched] "+s"(touched), [asg] "+v"(asg), [rcf] "+v"(rcf), [rmf] "+v"(rmf), [rcu] "+v"(rcu),
-          [nchk] "+s"(nchk), [ta] "=&s"(ta), [tb] "=&s"(tb), [ac] "=&s"(ac), [am] "=&s"(am), [ar] "=&s"(ar),
-          [ax] "=&s"(ax), [bc] "=&s"(bc), [bm] "=&s"(bm), [br] "=&s"(br), [bx] "=&s"(bx), [l] "=&s"(l),
-          [nv] "=&s"(nv), [m2] "=&s"(m2), [esv] "=&s"(esv), [t0] "=&v"(t0)
-        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [gbg] "s"(gbg)
-        : "scc", "vcc", "memory");
-#undef FGY_ONE
-}
-
-template <uint32_t g, uint32_t G>
-__device__ __forceinline__ void fpp_group_y(uint64_t q, uint64_t &placed, uint64_t &touched, uint32_t &asg,
-                                            uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
-                                            uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
-                                            uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
-                                            uint32_t &nhit) {
-    fpp_asm_group_y(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
-    const uint32_t lane = __lane_id();
-    const bool inq = (q >> lane) & 1ull;
-    const uint64_t hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);
-#ifdef FP_PIPE_STATS
-    nhit += (uint32_t)__builtin_popcountll(hit);
-#else
-    (void)nhit;
-#endif
-    placed |= hit;
-    if (inq && asg == 0xFFFFFFFFu) {
-        const uint64_t above = (((uint64_t)cand_hi << 32) | cand) & ~((2ull << g) - 1ull);
-        nxt = above ? (uint32_t)__builtin_ctzll(above) : G;
-    }
-}
-
-// fpp_asm_group_z: the exec-masked check / place of fpp_asm_group_x, software pipelined two
-// containers per iteration (the next container's readlanes fill the v_cmp -> s_and
-// latency), the assignment written as the bare node lane (v_writelane; the caller adds the
-// group base), one loop branch per two containers.  Counts per container: 21 instructions.
-__device__ __forceinline__ void fpp_asm_group_z(uint64_t q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
-                                                uint32_t &rmf, uint32_t &rcu, uint32_t rlab, uint32_t cpu,
-                                                uint32_t mem, uint32_t req, uint32_t conf, uint32_t &nchk) {
-    uint32_t ta, tb, ac, am, ar, ax, bc, bm, br, bx, l, cnt, m0sv;
-    uint64_t m1, m2, m3, esv;
-    uint32_t t0;
-#define FGZ_ONE(T, KC, KM, KR, KX, TN, NC, NM, NR, NX)                                     \
-        "v_cmp_ge_u32_e64 %[m1], %[rcf], %[" KC "]\n\t"                                  \
-        "v_cmp_ge_u32_e64 %[m2], %[rmf], %[" KM "]\n\t"                                  \
-        "v_and_b32_e32 %[t0], %[" KR "], %[rlab]\n\t"                                    \
-        "v_and_or_b32 %[t0], %[rcu], %[" KX "], %[t0]\n\t"                               \
-        "v_cmp_eq_u32_e64 %[m3], 0, %[t0]\n\t"                                           \
-        "s_ff1_i32_b64 %[" TN "], %[q]\n\t"                                              \
-        "s_bitset0_b64 %[q], %[" TN "]\n\t"                                              \
-        "v_readlane_b32 %[" NC "], %[cpu], %[" TN "]\n\t"                                \
-        "s_and_b64 %[m1], %[m1], %[m2]\n\t"                                              \
-        "v_readlane_b32 %[" NM "], %[mem], %[" TN "]\n\t"                                \
-        "s_and_b64 %[m1], %[m1], %[m3]\n\t"                                              \
-        "v_readlane_b32 %[" NR "], %[req], %[" TN "]\n\t"                                \
-        "s_ff1_i32_b64 %[l], %[m1]\n\t"                                                  \
-        "v_readlane_b32 %[" NX "], %[conf], %[" TN "]\n\t"                               \
-        "s_lshl_b64 %[m2], 1, %[l]\n\t"                                                  \
-        "s_mov_b32 m0, %[" T "]\n\t"                                                     \
-        "s_and_b64 exec, %[m2], %[m1]\n\t"                                               \
-        "v_subrev_u32_e32 %[rcf], %[" KC "], %[rcf]\n\t"                                 \
-        "v_subrev_u32_e32 %[rmf], %[" KM "], %[rmf]\n\t"                                 \
-        "v_or_b32_e32 %[rcu], %[" KX "], %[rcu]\n\t"                                     \
-        "s_or_b64 %[touched], %[touched], exec\n\t"                                      \
-        "s_mov_b64 exec, %[esv]\n\t"                                                     \
-        "v_writelane_b32 %[asg], %[l], m0\n\t"
-    asm volatile(
-        "s_cmp_eq_u64 %[q], 0\n\t"
-        "s_cbranch_scc1 .Lfgz_end%=\n\t"
-        "s_mov_b32 %[m0sv], m0\n\t"
-        "s_mov_b64 %[esv], exec\n\t"
-        "s_bcnt1_i32_b64 %[cnt], %[q]\n\t"
-        "s_ff1_i32_b64 %[ta], %[q]\n\t"
-        "s_bitset0_b64 %[q], %[ta]\n\t"
-        "v_readlane_b32 %[ac], %[cpu], %[ta]\n\t"
-        "v_readlane_b32 %[am], %[mem], %[ta]\n\t"
-        "v_readlane_b32 %[ar], %[req], %[ta]\n\t"
-        "v_readlane_b32 %[ax], %[conf], %[ta]\n\t"
-        "s_lshr_b32 %[cnt], %[cnt], 1\n\t"           // pairs; bit 0 of the count is redone below
-        "s_cmp_eq_u32 %[cnt], 0\n\t"
-        "s_cbranch_scc1 .Lfgz_tail%=\n"
-        ".Lfgz_loop%=:\n\t"
-        FGZ_ONE("ta", "ac", "am", "ar", "ax", "tb", "bc", "bm", "br", "bx")
-        "s_nop 1\n\t"
-        FGZ_ONE("tb", "bc", "bm", "br", "bx", "ta", "ac", "am", "ar", "ax")
-        "s_sub_u32 %[cnt], %[cnt], 1\n\t"
-        "s_cmp_lg_u32 %[cnt], 0\n\t"
-        "s_cbranch_scc1 .Lfgz_loop%=\n"
-        ".Lfgz_tail%=:\n\t"
-        // an odd container left: ta >= 0 (the last prefetch found one)
-        "s_cmp_lt_i32 %[ta], 0\n\t"
-        "s_cbranch_scc1 .Lfgz_done%=\n\t"
-        FGZ_ONE("ta", "ac", "am", "ar", "ax", "tb", "bc", "bm", "br", "bx")
-        ".Lfgz_done%=:\n\t"
-        "s_mov_b32 m0, %[m0sv]\n"
-        ".Lfgz_end%=:"
-        : [q] "+s"(q), [touched] "+s"(touched), [asg] "+v"(asg), [rcf] "+v"(rcf), [rmf] "+v"(rmf), [rcu] "+v"(rcu),
-          [nchk] "+s"(nchk), [ta] "=&s"(ta), [tb] "=&s"(tb), [ac] "=&s"(ac), [am] "=&s"(am), [ar] "=&s"(ar),
-          [ax] "=&s"(ax), [bc] "=&s"(bc), [bm] "=&s"(bm), [br] "=&s"(br), [bx] "=&s"(bx), [l] "=&s"(l),
-          [cnt] "=&s"(cnt), [m0sv] "=&s"(m0sv), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [esv] "=&s"(esv),
-          [t0] "=&v"(t0)
-        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf)
-        : "scc", "memory");
-#undef FGZ_ONE
-}
-
-template <uint32_t g, uint32_t G>
-__device__ __forceinline__ void fpp_group_z(uint64_t q, uint64_t &placed, uint64_t &touched, uint32_t &asg,
-                                            uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
-                                            uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
-                                            uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
-                                            uint32_t &nhit) {
-    fpp_asm_group_z(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, nchk);
-    const uint32_t lane = __lane_id();
-    const bool inq = (q >> lane) & 1ull;
-    const bool hit = inq && asg != 0xFFFFFFFFu;
-    const uint64_t hm = __builtin_amdgcn_ballot_w64(hit);
-#ifdef FP_PIPE_STATS
-    nhit += (uint32_t)__builtin_popcountll(hm);
-#else
-    (void)nhit;
-#endif
-    placed |= hm;
-    if (hit) asg |= gb64 + g * 64u;
-    if (inq && !hit) {
-        const uint64_t above = (((uint64_t)cand_hi << 32) | cand) & ~((2ull << g) - 1ull);
-        nxt = above ? (uint32_t)__builtin_ctzll(above) : G;
-    }
-}
-
 }  // namespace fpp
