@@ -1012,10 +1012,8 @@ __global__ void k_cost_reduce(uint32_t S, uint32_t B, uint32_t scen_base, const 
 // field, if any, is masked off; c/m are the values, or their dense ranks decoded through
 // the value tables cval/mval), so only req, conf and level are gathered at random;
 // without keys (all-zero or all-equal demands) everything is.
-// XCD-aware: blocks b and b + 8 share an XCD (round-robin dispatch), so logical block
-// (b % 8) * (grid / 8) + b / 8 gives each XCD a contiguous eighth of every grid-stride
-// pass -- about ten config-4 scenarios, whose random req/conf reads then stay in that
-// XCD's 4 MB L2 instead of being fetched by all eight.
+// The buckets of both demands (one binary search over the thresholds, in LDS) ride in the
+// position word when positions fit 21 bits (PipeArgs::kpack).
 // bucket thresholds for k_gather_sorted (by value: [0, K) cpu, [K, 2K) mem)
 struct GatherThr {
     uint32_t t[2 * K];
@@ -1033,8 +1031,12 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
                                 uint32_t *__restrict__ s_conf, uint32_t *__restrict__ s_idx) {
     // S * C < 2^32 (fp_dev_place_batch_impl checks): 32-bit index arithmetic, and four
     // independent elements per thread in flight (the req/conf gathers are dependent loads)
-    const uint32_t total = S * C, stride = gridDim.x * blockDim.x;
+    const uint32_t total = S * C;
+    // one tile of 4 x blockDim contiguous elements per block; blocks b and b + 8 share an XCD, so
+    // the XCD-contiguous tile order below keeps each XCD's running blocks inside ~5 config-4
+    // scenarios at a time (their random req/conf/level lines fit its 4 MB L2)
     const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t stride = blockDim.x;
     __shared__ uint32_t T[2 * K];
     if (threadIdx.x < 2 * K) T[threadIdx.x] = th.t[threadIdx.x];
     __syncthreads();
@@ -1045,7 +1047,8 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
         for (uint32_t step = K / 2; step; step >>= 1) k += t[k + step] <= v ? step : 0u;
         return k;
     };
-    for (size_t i0 = (size_t)lb * blockDim.x + threadIdx.x; i0 < total; i0 += 4 * (size_t)stride) {
+    {
+        const size_t i0 = (size_t)lb * 4 * blockDim.x + threadIdx.x;
         uint32_t j[4], src[4], r[4], f[4], cy[4], cv[4], mv[4], pos[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1372,8 +1375,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     memcpy(gth.t + K, tm, sizeof(uint32_t) * K);
     gth.kpack = kpack;
     {
-        size_t g = (SC + 1023) / 1024;  // four elements per thread per pass
-        if (g > 16384) g = 16384;
+        size_t g = (SC + 1023) / 1024;  // one tile of 1024 elements per block
         if (g >= 64) g = (g + 7) & ~(size_t)7;  // a multiple of 8: XCD-contiguous mapping
         if (key_bytes == 4)
             k_gather_sorted<uint32_t><<<(unsigned)g, 256, 0, st>>>(
