@@ -81,10 +81,19 @@ int fp_place_ws_bytes_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint64
 // bucket thresholds of the candidate masks: K ascending values, T[0] = 0
 constexpr int FP_BUCKETS = 32;
 void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T);  // geometric from lo to hi
+// the FFD-sorted SoA [S][C] the pipeline streams (fp_pipe.hip)
+struct fp_pipe_soa {
+    uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;
+};
+int fp_pipe_soa_take(fp_ctx *c, size_t SC, fp_pipe_soa *soa);
+// 1 when the position word carries the bucket indices (bits 21-30)
+uint32_t fp_pipe_kpack(uint32_t C);
+// ready: the per-scenario LDS sort already wrote order, s_cpu, s_mem and s_idx (only the
+// req / conf / CYCLE gather remains); null: gather everything from order + sorted keys
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
                    const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
-                   const uint32_t *tm);
+                   const uint32_t *tm, const fp_pipe_soa *ready);
 
 // ---- device helpers ----
 namespace fpd {

@@ -1102,6 +1102,42 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
     }
 }
 
+// The rest of the sorted SoA after k_scen_sort (fp_place.hip) wrote order, cpu, mem and the
+// position word: req and conf gathered at random (same XCD-contiguous tiles as
+// k_gather_sorted, so an XCD's random lines stay in its L2) and the CYCLE bit from level.
+__global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
+                                 const uint32_t *__restrict__ req, const uint32_t *__restrict__ conf,
+                                 const uint32_t *__restrict__ level, uint32_t *__restrict__ s_req,
+                                 uint32_t *__restrict__ s_conf, uint32_t *__restrict__ s_idx) {
+    const uint32_t total = S * C;
+    const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t i0 = lb * 4 * blockDim.x + threadIdx.x;
+    uint32_t src[4], r[4], f[4], cy[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < total) src[u] = i - i % C + __builtin_nontemporal_load(&order[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < total) {
+            r[u] = req[src[u]];
+            f[u] = conf[src[u]];
+            cy[u] = (level && level[src[u]] == FP_NONE) ? CYC : 0u;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < total) {
+            __builtin_nontemporal_store(r[u], &s_req[i]);
+            __builtin_nontemporal_store(f[u], &s_conf[i]);
+            if (level && cy[u]) s_idx[i] |= CYC;
+        }
+    }
+}
+
 // assign/reason from FFD (sorted) order back to container order, per scenario and per
 // range of container indices held in LDS: every read and write is coalesced.  The
 // pipeline's stores hit the sorted arrays at positions that advance together, so its
@@ -1342,10 +1378,23 @@ size_t fp_pipe_ws_bytes(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N) {
            10 * 256;
 }
 
+uint32_t fp_pipe_kpack(uint32_t C) {
+    return C <= (IDX_POS_MASK + 1u) && !(getenv("FLEETPLACE_NO_KPACK") && atoi(getenv("FLEETPLACE_NO_KPACK")));
+}
+
+int fp_pipe_soa_take(fp_ctx *c, size_t SC, fp_pipe_soa *soa) {
+    soa->s_cpu = (uint32_t *)fp_ws_take(c, SC * 4);
+    soa->s_mem = (uint32_t *)fp_ws_take(c, SC * 4);
+    soa->s_req = (uint32_t *)fp_ws_take(c, SC * 4);
+    soa->s_conf = (uint32_t *)fp_ws_take(c, SC * 4);
+    soa->s_idx = (uint32_t *)fp_ws_take(c, SC * 4);
+    return (soa->s_cpu && soa->s_mem && soa->s_req && soa->s_conf && soa->s_idx) ? FP_OK : FP_ENOMEM;
+}
+
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
                    const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
-                   const uint32_t *tm) {
+                   const uint32_t *tm, const fp_pipe_soa *ready) {
     PipeGeom geo;
     if (!pipe_geom(c, S, C, N, &geo)) return FP_EOVERFLOW;
     const uint32_t G = geo.G, W = geo.W, B = geo.B, R = geo.R, slots = geo.slots;
@@ -1355,26 +1404,30 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;
     const size_t nlinks = (size_t)S * (B - 1);
-    uint32_t *s_cpu = (uint32_t *)fp_ws_take(c, SC * 4);
-    uint32_t *s_mem = (uint32_t *)fp_ws_take(c, SC * 4);
-    uint32_t *s_req = (uint32_t *)fp_ws_take(c, SC * 4);
-    uint32_t *s_conf = (uint32_t *)fp_ws_take(c, SC * 4);
-    uint32_t *s_idx = (uint32_t *)fp_ws_take(c, SC * 4);
+    fp_pipe_soa soa;
+    if (ready) soa = *ready;
+    else if (int rc0 = fp_pipe_soa_take(c, SC, &soa)) return rc0;
+    uint32_t *s_cpu = soa.s_cpu, *s_mem = soa.s_mem, *s_req = soa.s_req, *s_conf = soa.s_conf, *s_idx = soa.s_idx;
     uint32_t *ctl = (uint32_t *)fp_ws_take(c, 256 + nlinks * LCTL * 4);  // ticket, abort | link control
     uint32_t *part = (uint32_t *)fp_ws_take(c, (size_t)S * B * 8 + 8);
     uint32_t *gdata = nlinks ? (uint32_t *)fp_ws_take(c, nlinks * slots * 2 * 64 * 4) : nullptr;
     uint32_t *asg_s = (uint32_t *)fp_ws_take(c, SC * 4);  // plan in FFD order (k_unsort input)
     uint8_t *rsn_s = (uint8_t *)fp_ws_take(c, SC);
-    if (!s_cpu || !s_mem || !s_req || !s_conf || !s_idx || !ctl || !part || (nlinks && !gdata) || !asg_s || !rsn_s)
-        return FP_ENOMEM;
+    if (!ctl || !part || (nlinks && !gdata) || !asg_s || !rsn_s) return FP_ENOMEM;
     FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * LCTL * 4, st));
     // buckets ride in s_idx when positions fit 21 bits (FLEETPLACE_NO_KPACK=1: search per stage)
-    const uint32_t kpack = C <= (IDX_POS_MASK + 1u) && !(getenv("FLEETPLACE_NO_KPACK") && atoi(getenv("FLEETPLACE_NO_KPACK")));
+    const uint32_t kpack = fp_pipe_kpack(C);
     GatherThr gth;
     memcpy(gth.t, tc, sizeof(uint32_t) * K);
     memcpy(gth.t + K, tm, sizeof(uint32_t) * K);
     gth.kpack = kpack;
-    {
+    if (ready) {  // k_scen_sort wrote order, cpu, mem and the position words
+        size_t g = (SC + 1023) / 1024;
+        if (g >= 64) g = (g + 7) & ~(size_t)7;
+        k_gather_payload<<<(unsigned)g, 256, 0, st>>>(S, C, order, b->req_labels, b->conflict, b->level, s_req,
+                                                      s_conf, s_idx);
+        FP_HIP(hipGetLastError());
+    } else {
         size_t g = (SC + 1023) / 1024;  // one tile of 1024 elements per block
         if (g >= 64) g = (g + 7) & ~(size_t)7;  // a multiple of 8: XCD-contiguous mapping
         if (key_bytes == 4)

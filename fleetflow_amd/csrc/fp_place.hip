@@ -232,6 +232,335 @@ __global__ void k_argmin_cost(const uint64_t *__restrict__ cost, uint32_t n, uin
     }
 }
 
+// ---- per-scenario LDS sort (scenarios of at most ~50k containers) ----
+//
+// Every scenario is sorted into FFD order (cpu desc, mem desc, index asc) by one workgroup
+// of 1024 threads in LDS.  It writes the order and the sorted cpu / mem / position words
+// itself, so no radix keys, onesweep passes or key decode touch HBM.  The digits are dense
+// value ranks, flipped so that an ascending digit means a descending demand:
+// hd = dc-1-rank(cpu), ld = dm-1-rank(mem), each below 256.
+//   k_digits   streaming pass at full occupancy (rank tables staged in LDS): one u16
+//              digit pair per container (hd | ld << 8)
+//   k_scen_sort, one workgroup per scenario:
+//     A0  wave w counts the hd digits of its contiguous slice of the scenario (packed u16
+//         LDS atomics) and keeps ld[j] in LDS; one scan gives every (wave, digit) its offset
+//     A1  each wave walks its slice in order, 64 containers at a time; a container's place
+//         among equal digits in the 64 is a match mask of ballots, so X[p] = index in
+//         stable hd order with no barrier inside the pass
+//     B   every hd bucket (~630 containers in config 4) is sorted by ld by one wave, stable
+//         the same way, and written straight to its final positions; the bucket's window of
+//         each output array is a few KB, so its scattered dword stores merge in L2
+// LDS: X u16[C] + ld u8[C] + [16][256] u16 + tables (~11.5 KB) -> C <= ~50.7k.
+constexpr uint32_t SS_DIG = 256;     // digits per dimension (dense ranks)
+constexpr uint32_t SS_WAVES = 16;
+constexpr uint32_t SS_BATCH = 8;     // digit loads in flight per lane in A0 / A1
+constexpr uint32_t SS_REG = 16;      // B: buckets of up to 64 x SS_REG containers are reordered in registers
+constexpr size_t SS_LDS_CAP = 160 * 1024;
+constexpr uint32_t DG_TABLE_WORDS = 4096;  // k_digits stages rank tables of at most this many words in LDS
+
+__host__ __device__ static inline size_t ss_align16(size_t b) { return (b + 15) & ~(size_t)15; }
+// X, LD, WH [16][256] u16, HS/HB u32 [256], MV u32 [256], MB/CB u8 [256], NEXT
+static inline size_t ss_lds_bytes(uint32_t C) {
+    return ss_align16((size_t)C * 2) + ss_align16(C) + SS_WAVES * SS_DIG * 2 + 2 * SS_DIG * 4 + SS_DIG * 4 +
+           2 * SS_DIG + 16;
+}
+
+// u16 digit pair per container: hd | ld << 8 (dense ranks, ascending = descending demand)
+__global__ __launch_bounds__(256) void k_digits(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
+                                                size_t n, uint32_t dc, uint32_t dm, uint32_t wc, uint32_t wm,
+                                                const uint32_t *__restrict__ bmc, const uint32_t *__restrict__ prc,
+                                                const uint32_t *__restrict__ bmm, const uint32_t *__restrict__ prm,
+                                                uint16_t *__restrict__ dig) {
+    extern __shared__ uint32_t dgt[];  // [wc] bm, [wc] pre (cpu), [wm] bm, [wm] pre (mem) when they fit
+    const bool lds = wc + wm <= DG_TABLE_WORDS;
+    if (lds) {
+        for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) { dgt[i] = bmc[i]; dgt[wc + i] = prc[i]; }
+        for (uint32_t i = threadIdx.x; i < wm; i += blockDim.x) { dgt[2 * wc + i] = bmm[i]; dgt[2 * wc + wm + i] = prm[i]; }
+        __syncthreads();
+    }
+    const uint32_t *tbc = lds ? dgt : bmc, *tpc = lds ? dgt + wc : prc;
+    const uint32_t *tbm = lds ? dgt + 2 * wc : bmm, *tpm = lds ? dgt + 2 * wc + wm : prm;
+    auto digit = [&](uint32_t c, uint32_t m) -> uint32_t {
+        const uint32_t rc = tpc[c >> 5] + (uint32_t)__popc(tbc[c >> 5] & ((1u << (c & 31)) - 1u));
+        const uint32_t rm = tpm[m >> 5] + (uint32_t)__popc(tbm[m >> 5] & ((1u << (m & 31)) - 1u));
+        return (dc - 1u - rc) | ((dm - 1u - rm) << 8);
+    };
+    const size_t stride = (size_t)gridDim.x * blockDim.x, t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t head = 0;
+    if (((reinterpret_cast<uintptr_t>(cpu) | reinterpret_cast<uintptr_t>(mem)) & 15u) == 0 &&
+        (reinterpret_cast<uintptr_t>(dig) & 7u) == 0) {
+        const uint4 *c4 = reinterpret_cast<const uint4 *>(cpu), *m4 = reinterpret_cast<const uint4 *>(mem);
+        uint2 *d4 = reinterpret_cast<uint2 *>(dig);
+        for (size_t i = t; i < n / 4; i += stride) {
+            const uint4 c = c4[i], m = m4[i];
+            uint2 o;
+            o.x = digit(c.x, m.x) | (digit(c.y, m.y) << 16);
+            o.y = digit(c.z, m.z) | (digit(c.w, m.w) << 16);
+            d4[i] = o;
+        }
+        head = n / 4 * 4;
+    }
+    for (size_t i = head + t; i < n; i += stride) dig[i] = (uint16_t)digit(cpu[i], mem[i]);
+}
+
+struct ScenSortArgs {
+    uint32_t C, dc, dm, kpack;
+    const uint16_t *dig;                     // [S][C] k_digits
+    const uint32_t *cval, *mval;             // ascending distinct values
+    uint32_t *order, *s_cpu, *s_mem, *s_idx; // [S][C] FFD order, sorted cpu / mem / position word
+    uint32_t T[2 * FP_BUCKETS];              // bucket thresholds (cpu, then mem)
+};
+
+// the u16 digit rows are also counted, zeroed and scanned through 32/64-bit views: these
+// types may alias the u16 entries (else type-based alias analysis may reorder them)
+typedef uint64_t __attribute__((may_alias)) ss_u64a;
+typedef uint32_t __attribute__((may_alias)) ss_u32a;
+
+// lanes holding the same digit as this lane (among `valid` lanes); digits < 2^nb
+__device__ __forceinline__ uint64_t ss_match(uint32_t v, bool valid, uint32_t nb) {
+    uint64_t m = __builtin_amdgcn_ballot_w64(valid);
+    for (uint32_t b = 0; b < nb; ++b) {
+        const bool bit = (v >> b) & 1u;
+        const uint64_t bb = __builtin_amdgcn_ballot_w64(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t ss_bucket(const uint32_t *t, uint32_t v) {
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t step = FP_BUCKETS / 2; step; step >>= 1) k += t[k + step] <= v ? step : 0u;
+    return k;
+}
+
+// +1 on the u16 counter `d` of a packed row (two counters per dword; counts stay < 2^16)
+__device__ __forceinline__ void ss_inc16(uint16_t *row, uint32_t d) {
+    atomicAdd(reinterpret_cast<ss_u32a *>(row) + (d >> 1), 1u << ((d & 1u) * 16u));
+}
+
+// exclusive scan of a 256-entry u16 row (4 entries per lane) from `base`, in place
+__device__ __forceinline__ void ss_row_scan(uint16_t *row, uint32_t lane, uint32_t base) {
+    const uint64_t q = reinterpret_cast<ss_u64a *>(row)[lane];
+    const uint32_t c0 = (uint32_t)(q & 0xFFFF), c1 = (uint32_t)((q >> 16) & 0xFFFF), c2 = (uint32_t)((q >> 32) & 0xFFFF);
+    const uint32_t sum = c0 + c1 + c2 + (uint32_t)(q >> 48);
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        inc += lane >= (uint32_t)o ? y : 0u;
+    }
+    const uint64_t e0 = base + inc - sum;
+    reinterpret_cast<ss_u64a *>(row)[lane] = e0 | ((e0 + c0) << 16) | ((e0 + c0 + c1) << 32) | ((e0 + c0 + c1 + c2) << 48);
+}
+
+__global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char ssm[];
+    const uint32_t C = a.C, dc = a.dc, dm = a.dm;
+    uint16_t *X = reinterpret_cast<uint16_t *>(ssm);
+    uint8_t *LD = ssm + ss_align16((size_t)C * 2);
+    uint16_t *WH = reinterpret_cast<uint16_t *>(LD + ss_align16(C));     // [wave][digit]
+    uint32_t *HS = reinterpret_cast<uint32_t *>(WH + SS_WAVES * SS_DIG);  // bucket starts
+    uint32_t *HB = HS + SS_DIG;                                          // bucket ends
+    uint32_t *MV = HB + SS_DIG;                                          // mem value per ld
+    uint8_t *MB = reinterpret_cast<uint8_t *>(MV + SS_DIG);              // mem bucket per ld
+    uint8_t *CB = MB + SS_DIG;                                           // cpu bucket per hd
+    uint32_t *NEXT = reinterpret_cast<uint32_t *>(CB + SS_DIG);
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const size_t cb = (size_t)blockIdx.x * C;
+    const uint16_t *dig = a.dig + cb;
+    const uint32_t hbits = 32u - (uint32_t)__builtin_clz(dc | 1u), lbits = 32u - (uint32_t)__builtin_clz(dm | 1u);
+
+    for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
+    if (t < SS_DIG) {
+        const uint32_t mv = t < dm ? a.mval[dm - 1u - t] : 0u;
+        MV[t] = mv;
+        MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, mv) : 0;
+        CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, a.cval[dc - 1u - t]) : 0;
+    }
+    if (t == 0) NEXT[0] = 0u;
+    __syncthreads();
+
+    // A0: per-wave hd counts over the wave's slice [s0, s1), ld into LDS
+    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
+    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
+    uint16_t *myrow = WH + w * SS_DIG;
+    for (uint32_t p0 = s0; p0 < s1; p0 += 64 * SS_BATCH) {  // SS_BATCH loads in flight per lane
+        uint32_t dv[SS_BATCH];
+#pragma unroll
+        for (uint32_t k = 0; k < SS_BATCH; ++k) {
+            const uint32_t p = p0 + 64 * k + lane;
+            dv[k] = p < s1 ? (uint32_t)__builtin_nontemporal_load(&dig[p]) : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SS_BATCH; ++k) {
+            const uint32_t p = p0 + 64 * k + lane;
+            if (p < s1) {
+                LD[p] = (uint8_t)(dv[k] >> 8);
+                ss_inc16(myrow, dv[k] & 0xFFu);
+            }
+        }
+    }
+    __syncthreads();
+#ifdef SS_STOP  // timing variants (tools/build_variant.sh): stop after phase N with an identity order
+    if (SS_STOP == 1) {
+        for (uint32_t i = t; i < C; i += blockDim.x) {
+            a.order[cb + i] = i; a.s_cpu[cb + i] = 1; a.s_mem[cb + i] = 1; a.s_idx[cb + i] = i;
+        }
+        return;
+    }
+#endif
+    if (t < SS_DIG) {  // totals per digit (thread t = digit t)
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t ww = 0; ww < SS_WAVES; ++ww) s += WH[ww * SS_DIG + t];
+        HB[t] = s;
+    }
+    __syncthreads();
+    if (w == 0) {  // bucket starts: exclusive scan of the totals (4 per lane)
+        const uint32_t c0 = HB[4 * lane], c1 = HB[4 * lane + 1], c2 = HB[4 * lane + 2], c3 = HB[4 * lane + 3];
+        const uint32_t sum = c0 + c1 + c2 + c3;
+        uint32_t inc = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+            inc += lane >= (uint32_t)o ? y : 0u;
+        }
+        const uint32_t ex = inc - sum;
+        HS[4 * lane] = ex;
+        HS[4 * lane + 1] = ex + c0;
+        HS[4 * lane + 2] = ex + c0 + c1;
+        HS[4 * lane + 3] = ex + c0 + c1 + c2;
+    }
+    __syncthreads();
+    if (t < SS_DIG) {  // (wave, digit) offsets in wave order; HB = bucket ends
+        uint32_t run = HS[t];
+#pragma unroll
+        for (uint32_t ww = 0; ww < SS_WAVES; ++ww) {
+            const uint32_t c = WH[ww * SS_DIG + t];
+            WH[ww * SS_DIG + t] = (uint16_t)run;
+            run += c;
+        }
+        HB[t] = run;
+    }
+    __syncthreads();
+
+#ifdef SS_STOP  // timing variants (tools/build_variant.sh): stop after phase N with an identity order
+    if (SS_STOP == 2) {
+        for (uint32_t i = t; i < C; i += blockDim.x) {
+            a.order[cb + i] = i; a.s_cpu[cb + i] = 1; a.s_mem[cb + i] = 1; a.s_idx[cb + i] = i;
+        }
+        return;
+    }
+#endif
+    // A1: stable scatter by hd, each wave over its own slice
+    for (uint32_t p00 = s0; p00 < s1; p00 += 64 * SS_BATCH) {
+        uint32_t dv[SS_BATCH];
+#pragma unroll
+        for (uint32_t k = 0; k < SS_BATCH; ++k) {
+            const uint32_t p = p00 + 64 * k + lane;
+            dv[k] = p < s1 ? (uint32_t)dig[p] & 0xFFu : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SS_BATCH; ++k) {
+            const uint32_t p0 = p00 + 64 * k;
+            if (p0 >= s1) break;  // wave-uniform
+            const uint32_t p = p0 + lane;
+            const bool valid = p < s1;
+            const uint32_t d = dv[k];
+            const uint64_t m = ss_match(d, valid, hbits);
+            const uint32_t off = myrow[d];
+            if (valid) {
+                if ((m & lt) == 0) myrow[d] = (uint16_t)(off + __popcll(m));
+                X[off + (uint32_t)__popcll(m & lt)] = (uint16_t)p;
+            }
+        }
+    }
+    __syncthreads();
+
+#ifdef SS_STOP  // timing variants (tools/build_variant.sh): stop after phase N with an identity order
+    if (SS_STOP == 3) {
+        for (uint32_t i = t; i < C; i += blockDim.x) {
+            a.order[cb + i] = i; a.s_cpu[cb + i] = 1; a.s_mem[cb + i] = 1; a.s_idx[cb + i] = i;
+        }
+        return;
+    }
+#endif
+    // B: each hd bucket sorted by ld by one wave and written out
+    while (true) {
+        uint32_t d = 0;
+        if (lane == 0) d = atomicAdd(NEXT, 1u);
+        d = (uint32_t)__shfl((int)d, 0);
+        if (d >= dc) break;
+        const uint32_t lo = HS[d], hi = HB[d];
+        if (lo == hi) continue;
+        // the row is zeroed, counted with atomics, scanned and consumed by the same wave: the
+        // fences keep those accesses in order (s_waitcnt lgkmcnt(0), no compiler reordering)
+        reinterpret_cast<ss_u64a *>(myrow)[lane] = 0ull;  // 4 digits per lane
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        const uint32_t cv = a.cval[dc - 1u - d];
+        const uint32_t kbc = a.kpack ? (uint32_t)CB[d] << 21 : 0u;
+        if (hi - lo <= 64 * SS_REG) {
+            // the bucket in registers: count, scan, reorder X[lo, hi) in place, then write the
+            // bucket's window of every output array coalesced
+            uint32_t jv[SS_REG], lv[SS_REG];
+#pragma unroll
+            for (uint32_t k = 0; k < SS_REG; ++k) {
+                const uint32_t p = lo + 64 * k + lane;
+                jv[k] = p < hi ? X[p] : 0u;
+                lv[k] = p < hi ? LD[jv[k]] : 0u;
+                if (p < hi) ss_inc16(myrow, lv[k]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            ss_row_scan(myrow, lane, lo);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll
+            for (uint32_t k = 0; k < SS_REG; ++k) {
+                if (lo + 64 * k >= hi) break;  // wave-uniform
+                const bool valid = lo + 64 * k + lane < hi;
+                const uint64_t m = ss_match(lv[k], valid, lbits);
+                const uint32_t off = myrow[lv[k]];
+                if (valid) {
+                    if ((m & lt) == 0) myrow[lv[k]] = (uint16_t)(off + __popcll(m));
+                    X[off + (uint32_t)__popcll(m & lt)] = (uint16_t)jv[k];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            for (uint32_t P = lo + lane; P < hi; P += 64) {
+                const uint32_t j = X[P], l = LD[j];
+                a.order[cb + P] = j;
+                a.s_cpu[cb + P] = cv;
+                a.s_mem[cb + P] = MV[l];
+                a.s_idx[cb + P] = P | kbc | (a.kpack ? (uint32_t)MB[l] << 26 : 0u);
+            }
+        } else {  // a large bucket: the same stable order, scattered straight to HBM
+#pragma unroll 4
+            for (uint32_t p = lo + lane; p < hi; p += 64) ss_inc16(myrow, LD[X[p]]);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            ss_row_scan(myrow, lane, lo);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            for (uint32_t p0 = lo; p0 < hi; p0 += 64) {
+                const uint32_t p = p0 + lane;
+                const bool valid = p < hi;
+                const uint32_t j = valid ? X[p] : 0u;
+                const uint32_t l = valid ? LD[j] : 0u;
+                const uint64_t m = ss_match(l, valid, lbits);
+                const uint32_t off = myrow[l];
+                if (valid) {
+                    if ((m & lt) == 0) myrow[l] = (uint16_t)(off + __popcll(m));
+                    const uint32_t P = off + (uint32_t)__popcll(m & lt);
+                    a.order[cb + P] = j;
+                    a.s_cpu[cb + P] = cv;
+                    a.s_mem[cb + P] = MV[l];
+                    a.s_idx[cb + P] = P | kbc | (a.kpack ? (uint32_t)MB[l] << 26 : 0u);
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+}
+
 }  // namespace
 
 // T[0] = 0; T[1..31] spread evenly over the ascending distinct positive values v[0..d)
@@ -380,6 +709,47 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         cbits = fp_bitwidth(dc - 1);
         mbits = fp_bitwidth(dm - 1);
     }
+    // Per-scenario LDS sort: dense ranks with at most 256 values per dimension and a
+    // scenario that fits LDS (C <= 51k).  FLEETPLACE_NO_SCEN_SORT=1 keeps the radix path.
+    const bool scen_sort = ranks && dc >= 1 && dm >= 1 && dc <= SS_DIG && dm <= SS_DIG &&
+                           ss_lds_bytes(C) <= SS_LDS_CAP &&
+                           !(getenv("FLEETPLACE_NO_SCEN_SORT") && atoi(getenv("FLEETPLACE_NO_SCEN_SORT")));
+    if (scen_sort) {
+        uint32_t tc[FP_BUCKETS], tm[FP_BUCKETS];
+        {
+            std::vector<uint32_t> hv((size_t)dc + dm);
+            FP_HIP(hipMemcpyAsync(hv.data(), rval, (size_t)dc * 4, hipMemcpyDeviceToHost, st));
+            FP_HIP(hipMemcpyAsync(hv.data() + dc, rval + RANK_MAX_VALUE, (size_t)dm * 4, hipMemcpyDeviceToHost, st));
+            FP_HIP(hipStreamSynchronize(st));
+            value_thresholds(hv.data(), dc, tc);
+            value_thresholds(hv.data() + dc, dm, tm);
+        }
+        uint16_t *dig = (uint16_t *)keys_in;  // SC x u16 digit pairs (keys_in holds SC x 8 B)
+        {
+            const uint32_t wc = (maxc >> 5) + 1, wm = (maxm >> 5) + 1;
+            const size_t tl = wc + wm <= DG_TABLE_WORDS ? (size_t)(wc + wm) * 8 : 0;
+            FP_HIP(hipFuncSetAttribute((const void *)k_digits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
+            k_digits<<<grid_for((SC + 3) / 4, 256) < 4096 ? grid_for((SC + 3) / 4, 256) : 4096, 256, tl, st>>>(
+                b->cpu_m, b->mem_mib, SC, dc, dm, wc, wm, rbm, rpre, rbm + RANK_WORDS, rpre + RANK_WORDS, dig);
+            FP_HIP(hipGetLastError());
+        }
+        ScenSortArgs sa;
+        sa.C = C; sa.dc = dc; sa.dm = dm; sa.kpack = fp_pipe_kpack(C);
+        sa.dig = dig;
+        sa.cval = rval; sa.mval = rval + RANK_MAX_VALUE;
+        fp_pipe_soa soa;
+        if (int rs = fp_pipe_soa_take(c, SC, &soa)) return rs;
+        sa.order = vals_out; sa.s_cpu = soa.s_cpu; sa.s_mem = soa.s_mem; sa.s_idx = soa.s_idx;
+        memcpy(sa.T, tc, sizeof(tc));
+        memcpy(sa.T + FP_BUCKETS, tm, sizeof(tm));
+        const size_t lds = ss_lds_bytes(C);
+        FP_HIP(hipFuncSetAttribute((const void *)k_scen_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        k_scen_sort<<<S, 1024, lds, st>>>(sa);
+        FP_HIP(hipGetLastError());
+        fp_prof_end(c, FP_K_SORT, ev);
+        return fp_pipe_launch(c, S, C, N, b->scen_base, vals_out, nullptr, 4, 0, 0, 0, rval, rval + RANK_MAX_VALUE, b,
+                              tc, tm, &soa);
+    }
     const uint32_t kbits = cbits + mbits;
     const uint64_t cmax = cbits ? ((cbits == 64 ? ~0ull : ((1ull << cbits) - 1))) : 0ull;
     const uint64_t mmax = mbits ? ((1ull << mbits) - 1) : 0ull;
@@ -458,7 +828,8 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     }
 
     // ---- 4-5: placement + cost ----
-    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, cval, mval, b, tc, tm);
+    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, cval, mval, b, tc, tm,
+                          nullptr);
 }
 
 extern "C" int fp_dev_argmin_cost(fp_ctx *c, const uint64_t *cost, uint32_t n, uint32_t *best) {
