@@ -1105,6 +1105,8 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
 // The rest of the sorted SoA after k_scen_sort (fp_place.hip) wrote order, cpu, mem and the
 // position word: req and conf gathered at random (same XCD-contiguous tiles as
 // k_gather_sorted, so an XCD's random lines stay in its L2) and the CYCLE bit from level.
+// (Interleaving req/conf in k_digits for one 8-byte read per container: gather 2.18 ->
+// 1.68 ms, but k_digits 0.39 -> 1.05 ms.)
 __global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
                                  const uint32_t *__restrict__ req, const uint32_t *__restrict__ conf,
                                  const uint32_t *__restrict__ level, uint32_t *__restrict__ s_req,
@@ -1161,11 +1163,23 @@ __global__ __launch_bounds__(1024) void k_unsort(uint32_t C, uint32_t H, uint32_
     const uint32_t s = blockIdx.x / H, h = blockIdx.x % H;
     const uint32_t lo = h * span, hi = min(C, lo + span);
     const size_t cb = (size_t)s * C;
-    for (uint32_t p = threadIdx.x; p < C; p += blockDim.x) {
-        const uint32_t j = __builtin_nontemporal_load(&order[cb + p]);
-        if (j >= lo && j < hi) {
-            la[j - lo] = (A)__builtin_nontemporal_load(&asg_s[cb + p]);  // FP_NONE -> 0xFFFF when narrow
-            lr[j - lo] = __builtin_nontemporal_load(&rsn_s[cb + p]);
+    constexpr uint32_t U = 8;  // loads in flight per thread
+    for (uint32_t p0 = threadIdx.x; p0 < C; p0 += blockDim.x * U) {
+        uint32_t j[U], av[U];
+        uint8_t rv[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t p = p0 + u * blockDim.x;
+            j[u] = p < C ? __builtin_nontemporal_load(&order[cb + p]) : 0xFFFFFFFFu;
+            av[u] = p < C ? __builtin_nontemporal_load(&asg_s[cb + p]) : 0u;
+            rv[u] = p < C ? __builtin_nontemporal_load(&rsn_s[cb + p]) : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (j[u] >= lo && j[u] < hi) {
+                la[j[u] - lo] = (A)av[u];  // FP_NONE -> 0xFFFF when narrow
+                lr[j[u] - lo] = rv[u];
+            }
         }
     }
     __syncthreads();
@@ -1500,6 +1514,39 @@ extern "C" int fp_debug_pipe_timeline(unsigned long long *out) {
 extern "C" int fp_debug_stage_span(unsigned long long *out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_span), sizeof(unsigned long long) * SPAN_MAX * 8) != hipSuccess)
         return FP_EDEVICE;
+    return FP_OK;
+}
+// s_memtime ticks per s_memrealtime tick (100 MHz) over a ~2 ms spin: the shader clock
+__global__ void k_debug_clock(unsigned long long *out) {
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+    unsigned long long r1 = r0;
+    while (r1 - r0 < 200000) r1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) { out[0] = c1 - c0; out[1] = r1 - r0; }
+}
+extern "C" int fp_debug_clock_ghz(fp_ctx *c, double *ghz) {
+    unsigned long long *d = nullptr, h[2] = {0, 0};
+    if (hipMalloc(&d, 16) != hipSuccess) return FP_ENOMEM;
+    k_debug_clock<<<1, 64, 0, c->stream>>>(d);
+    const bool ok = hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+                    hipStreamSynchronize(c->stream) == hipSuccess;
+    (void)hipFree(d);
+    if (!ok || !h[1]) return FP_EDEVICE;
+    *ghz = (double)h[0] / (double)h[1] * 0.1;
+    return FP_OK;
+}
+// launch geometry fp_dev_place_batch picks for S x C x N: [0] G [1] W [2] B [3] R [4] lag
+// [5] link slots [6] bounded [7] resident segment slots on the device (occupancy x CUs)
+extern "C" int fp_debug_pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t *out) {
+    PipeGeom g;
+    if (!pipe_geom(c, S, C, N, &g)) return FP_EOVERFLOW;
+    int dev_cu = 0, occ = 0;
+    (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+    const bool wide = wide_g(g.W, g.G);
+    const void *fn = wide ? kKernelWide[g.G / 4] : kKernel[g.G];
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(g.W * 64), g.lds);
+    const uint32_t v[8] = {g.G, g.W, g.B, g.R, g.lag, g.slots, g.bounded, (uint32_t)(occ * dev_cu)};
+    memcpy(out, v, sizeof(v));
     return FP_OK;
 }
 extern "C" int fp_debug_pipe_stats(unsigned long long *out, int reset) {

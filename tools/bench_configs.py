@@ -1,5 +1,6 @@
 """Timings of BASELINE configs 2, 3 and 5 on one MI355X (device-resident inputs,
-HIP-event kernel times + wall time per call), next to the single-thread C oracle
+warm medians of the wall time per call and of the HIP-event kernel times of the same
+calls), next to the single-thread C oracle
 on the same inputs (checker + CPU baseline).  Writes one JSON line per config.
 
     python tools/bench_configs.py [--reps 3] [--no-cpu]
@@ -10,6 +11,7 @@ the oracle's before its time is reported.
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -44,23 +46,41 @@ def dev_batch_from(cont, nodes, dev, level=None):
     return db
 
 
-def time_place(p, db, reps):
-    snap = db.node_snapshot()
-    p.profile(False)
-    p.profile(True)
-    walls = []
+def warm_median(p, call, kids, reps, before=None):
+    """One untimed warm-up call, then `reps` timed calls: the median wall time and, per kernel
+    id, the median of the per-call HIP-event times (each call's own launches), so that a
+    kernel time never includes the cold first call and never exceeds its wall."""
+    if before:
+        before()
+    call()
+    p.sync()
+    for k in kids:  # drain the warm-up's pending event pairs (if profiling was on)
+        p.kernel_stats(k)
+    walls, ev = [], {k: [] for k in kids}
     for _ in range(reps):
-        db.restore_nodes(snap)
+        if before:
+            before()
         torch.cuda.synchronize()
+        p.profile(False)
+        p.profile(True)
         t0 = time.perf_counter()
-        p.dev_place_batch(db)
+        call()
         p.sync()
         walls.append(time.perf_counter() - t0)
-    k_ms, k_n = p.kernel_stats(FP_K_PLACE)
-    s_ms, s_n = p.kernel_stats(FP_K_SORT)
-    print("place walls (ms):", [round(w * 1e3, 3) for w in walls], "kernel", k_ms, k_n, "sort", s_ms, s_n,
+        for k in kids:
+            ms, n = p.kernel_stats(k)
+            ev[k].append(ms)  # the call's total event time for this kernel id
+    p.profile(False)
+    print("walls (ms):", [round(w * 1e3, 3) for w in walls], {k: [round(x, 3) for x in v] for k, v in ev.items()},
           file=sys.stderr)
-    return min(walls) * 1e3, k_ms / max(k_n, 1), s_ms / max(s_n, 1)
+    return statistics.median(walls) * 1e3, {k: statistics.median(v) for k, v in ev.items()}
+
+
+def time_place(p, db, reps):
+    snap = db.node_snapshot()
+    wall, ev = warm_median(p, lambda: p.dev_place_batch(db), (FP_K_PLACE, FP_K_SORT), reps,
+                           before=lambda: db.restore_nodes(snap))
+    return wall, ev[FP_K_PLACE], ev[FP_K_SORT]
 
 
 def check_plan(db, ea, er):
@@ -99,23 +119,13 @@ def levelize_config(p, dev, reps, cpu):
     level_t = torch.empty(V, dtype=torch.int32, device=dev)
     order_t = torch.empty(V, dtype=torch.int32, device=dev)
     ncyc_t = torch.zeros(1, dtype=torch.int32, device=dev)
-    p.profile(False)
-    p.profile(True)
-    walls = []
-    for _ in range(reps):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        p.dev_levelize(rp_t, col_t, hd_t, level_t, order_t, ncyc_t)
-        p.sync()
-        walls.append(time.perf_counter() - t0)
-    print("levelize walls (ms):", [round(w * 1e3, 3) for w in walls], file=sys.stderr)
-    k_ms, k_n = p.kernel_stats(FP_K_LEVEL)
+    wall, ev = warm_median(p, lambda: p.dev_levelize(rp_t, col_t, hd_t, level_t, order_t, ncyc_t), (FP_K_LEVEL,), reps)
     (el, eo, en), cpu_ms = cpu_time(lambda: O.levelize(rp, col, hd))
     ok = (np.array_equal(level_t.cpu().numpy().view(np.uint32), el) and
           np.array_equal(order_t.cpu().numpy().view(np.uint32), eo) and int(ncyc_t.item()) == en)
-    wall = min(walls)
+    wall /= 1e3
     out = {"config": "5a: levelize 1M-vertex DAG", "V": V, "E": E, "levels": int(el[el != 0xFFFFFFFF].max()) + 1,
-           "cycle_vertices": en, "bit_exact": bool(ok), "gpu_wall_ms": wall * 1e3, "levelize_gpu_ms": k_ms / max(k_n, 1),
+           "cycle_vertices": en, "bit_exact": bool(ok), "gpu_wall_ms": wall * 1e3, "levelize_gpu_ms": ev[FP_K_LEVEL],
            "vertices_edges_per_s": (V + E) / wall,
            "algorithmic_bytes": 16 * V + 12 * E + 4,
            "achieved_GBps": (16 * V + 12 * E + 4) / wall / 1e9}
@@ -131,18 +141,9 @@ def feas_config(p, dev, name, seed, C, N, reps, cpu, bitmap):
     first_t = torch.empty(C, dtype=torch.int32, device=dev)
     count_t = torch.empty(C, dtype=torch.int32, device=dev)
     bm_t = torch.empty(((C + 63) // 64) * N, dtype=torch.int64, device=dev) if bitmap else None
-    p.profile(False)
-    p.profile(True)
-    walls = []
-    for _ in range(reps):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        p.dev_feasibility(db, first_t, count_t, bm_t)
-        p.sync()
-        walls.append(time.perf_counter() - t0)
-    k_ms, k_n = p.kernel_stats(FP_K_FEAS)
-    kern_ms = k_ms / max(k_n, 1)
-    out = {"config": name, "C": C, "N": N, "bitmap": bitmap, "gpu_wall_ms": min(walls) * 1e3, "feas_kernel_ms": kern_ms,
+    wall, ev = warm_median(p, lambda: p.dev_feasibility(db, first_t, count_t, bm_t), (FP_K_FEAS,), reps)
+    kern_ms = ev[FP_K_FEAS]
+    out = {"config": name, "C": C, "N": N, "bitmap": bitmap, "gpu_wall_ms": wall, "feas_kernel_ms": kern_ms,
            "evals_per_s": C * N / (kern_ms / 1e3), "work_equiv_GBps": 16 * C * N / (kern_ms / 1e3) / 1e9,
            "bitmap_GBps": (((C + 63) // 64) * N * 8 / (kern_ms / 1e3) / 1e9) if bitmap else 0.0}
     if cpu:
@@ -158,7 +159,7 @@ def feas_config(p, dev, name, seed, C, N, reps, cpu, bitmap):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--only", default="2,3,5,f")
     args = ap.parse_args()

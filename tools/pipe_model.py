@@ -1,19 +1,27 @@
 """Latency model of k_ffd_pipe from the diagnostics build (per-stage s_memtime
-counters, libfleetplace_stats.so) for both bench legs; writes JSON that bench.py's
-roofline reports as `latency_model`.
+counters, libfleetplace_stats.so) for both bench legs.  Writes the JSON that
+bench.py's roofline reports as `latency_model` (profiles/pipe_model_latest.json)
+plus the raw per-stage counters.
 
-    FLEETPLACE_LIB=$PWD/fleetflow_amd/libfleetplace_stats.so python tools/pipe_model.py out.json
+    python tools/pipe_model.py [out.json]     (on the GPU box; builds nothing)
 
-Per leg: exact checks and placements per scenario, the candidate-loop cycles per
-check, the prescan cycles, the stage lifetime and the pipeline overlap
-(sum of the stages' busy cycles / one stage's lifetime).  The model:
-  kernel_ms = ceil(S / resident) x (checks x cycles_per_check + prescan) / overlap / cycles_per_ms
-i.e. the time of the sequential first-fit chain, not of any memory traffic."""
+config 4 (many scenarios, throughput-bound): every scenario's B segments each hold one
+of the device's resident segment slots (occupancy x CUs, fp_debug_pipe_geom) for the
+segment's lifetime (s_memtime from its start to the end of its stream).  With lag = S
+the segments of a scenario run phase by phase, so
+    model_ms = S x sum_b life_b / slots / clock
+and the busy share of a lifetime is the exact checks + prescans; the rest is input
+waits, forwarding and the per-batch bookkeeping.
+config 3 (one scenario, one-group stages): every container walks the stages in FFD order
+until a node of the stage fits it.  Reported: container-stage visits, exact checks,
+placements and the summed busy cycles over the launch's cycles (the average number of
+stages busy at once) -- the chain of exact checks at the placement frontier, not memory,
+sets the time.
+"""
 import ctypes as ct
 import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -23,15 +31,33 @@ import torch  # noqa: E402
 
 from fleetflow_amd import DevBatch, Planner, _lib  # noqa: E402
 
-# (leg, scenarios in the diagnostics run, C, N, seed, scenarios resident at once on 256 CUs)
-LEGS = [("config4", int(os.environ.get("S_DIAG", 768)), 50_000, 5_000, 0x5EED0004, 768),
-        ("config3", 1, 1_000_000, 100_000, 0x5EED0003, 1)]
+# (leg, scenarios in the diagnostics run, C, N, seed)
+LEGS = [("config4", int(os.environ.get("S_DIAG", 4096)), 50_000, 5_000, 0x5EED0004),
+        ("config3", 1, 1_000_000, 100_000, 0x5EED0003)]
+
+
+def geom(p, S, C, N):
+    L = _lib.load()
+    f = L.fp_debug_pipe_geom
+    f.argtypes = [ct.c_void_p, ct.c_uint32, ct.c_uint32, ct.c_uint32, ct.POINTER(ct.c_uint32)]
+    out = (ct.c_uint32 * 8)()
+    assert f(p._ctx, S, C, N, out) == 0
+    return dict(zip(["G", "W", "B", "R", "lag", "link_slots", "bounded", "resident_segments"], list(out)))
+
+
+def clock_ghz(p):
+    L = _lib.load()
+    f = L.fp_debug_clock_ghz
+    f.argtypes = [ct.c_void_p, ct.POINTER(ct.c_double)]
+    v = ct.c_double()
+    assert f(p._ctx, ct.byref(v)) == 0
+    return v.value
 
 
 def measure(p, S, C, N, seed):
     db = DevBatch.allocate(S, C, N, "cuda:0")
     p.dev_gen_batch(seed, db, 7)
-    p.sync()  # the generator runs on the planner stream; torch copies on its own
+    p.sync()
     pristine = db.node_snapshot()
     torch.cuda.synchronize()
     L = _lib.load()
@@ -47,47 +73,60 @@ def measure(p, S, C, N, seed):
         p.dev_place_batch(db)
         p.sync()
     ms, n = p.kernel_stats(_lib.FP_K_PLACE)
-    print(f"  S={S} placed/scenario {int((db.reason == 0).sum().item()) / S:.0f}", flush=True)
+    placed = int((db.reason == 0).sum().item())
     f(buf, 0)
     v = [[buf[w * 16 + i] for i in range(16)] for w in range(16)]
-    v = [r for r in v if any(r)]
     del db, pristine
     torch.cuda.empty_cache()
-    return ms / n, v  # last launch's counters (reset before it); time = mean of both
+    return ms / n, placed, [r for r in v if any(r)]  # counters of the last launch (reset before it)
 
 
 def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pipe_model.json")
     p = Planner(0)
-    res = {}
-    for leg, S, C, N, seed, resident in LEGS:
-        kms, v = measure(p, S, C, N, seed)
-        checks = sum(r[1] for r in v) / S
-        hits = sum(r[2] for r in v) / S
-        cand = sum(r[10] for r in v) / S
-        pre = sum(r[9] for r in v) / S
-        # r[13] (whole loop) of stage slot w is summed over the scenario's segments
-        life_sum = max(r[13] for r in v) / S
-        stages = len(v)
-        res[leg] = {"S_diag": S, "C": C, "N": N, "resident_scenarios": resident,
-                    "stage_slots": stages, "kernel_ms_diag_build": kms,
-                    "checks_per_scenario": checks, "placements_per_scenario": hits,
-                    "cycles_per_check": cand / max(checks, 1), "cand_loop_cycles_per_scenario": cand,
-                    "prescan_cycles_per_scenario": pre,
-                    "stage_lifetime_cycles_summed_over_segments": life_sum,
-                    "miss_reasons_per_scenario": {"cap_ok_label_or_conflict": sum(r[6] for r in v) / S,
-                                                  "cap_label_ok_conflict": sum(r[7] for r in v) / S,
-                                                  "cpu_ok_mem_fails": sum(r[14] for r in v) / S,
-                                                  "mem_ok_cpu_fails": sum(r[15] for r in v) / S,
-                                                  "note": "C++ loop diagnostics build only (FP_NO_ASM)"},
-                    "per_stage": [{"visits": r[0] / S, "checks": r[1] / S, "hits": r[2] / S,
-                                   "cand_Mcycles": r[10] / S / 1e6, "prescan_Mcycles": r[9] / S / 1e6,
-                                   "input_Mcycles": r[8] / S / 1e6, "spin_in_per_batch": r[4] / max(r[3], 1),
-                                   "fwd_Mcycles": r[11] / S / 1e6, "batches": r[3] / S,
-                                   "life_Mcycles": r[13] / S / 1e6} for r in v]}
-        print(leg, json.dumps(res[leg]), flush=True)
+    clk = clock_ghz(p)
+    latest, raw = {}, {"clock_ghz": clk}
+    for leg, S, C, N, seed in LEGS:
+        g = geom(p, S, C, N)
+        kms, placed, v = measure(p, S, C, N, seed)
+        per = lambda i: sum(r[i] for r in v) / S  # noqa: E731  per scenario
+        checks, hits, visits = per(1), per(2), per(0)
+        busy = per(9) + per(10)
+        raw[leg] = {"geometry": g, "kernel_ms_diag_build": kms, "placed": placed,
+                    "per_stage_slot": [{"visits": r[0] / S, "checks": r[1] / S, "hits": r[2] / S, "batches": r[3] / S,
+                                        "input_Mcycles": r[8] / S / 1e6, "prescan_Mcycles": r[9] / S / 1e6,
+                                        "cand_Mcycles": r[10] / S / 1e6, "fwd_Mcycles": r[11] / S / 1e6,
+                                        "out_wait_Mcycles": r[12] / S / 1e6, "life_Mcycles": r[13] / S / 1e6}
+                                       for r in v]}
+        m = {"C": C, "N": N, "S_diag": S, "source": "tools/pipe_model.py, diagnostics build (libfleetplace_stats.so)",
+             "geometry": g, "clock_ghz": clk, "kernel_ms_diag_build": kms,
+             "container_stage_visits_per_scenario": visits, "checks_per_scenario": checks,
+             "placements_per_scenario": hits, "busy_cycles_per_scenario": busy,
+             "cycles_per_check": per(10) / max(checks, 1)}
+        if leg == "config4":
+            life = [r[13] / S for r in v]  # stats slot = segment b (B x W <= 16)
+            slots = g["resident_segments"]
+            m.update({"segments": g["B"], "slots": slots, "segment_life_cycles": life,
+                      "slot_cycles_per_scenario": sum(life), "busy_share": busy / max(sum(life), 1),
+                      "formula": "kernel_ms = S x slot_cycles_per_scenario / slots / clock: every scenario holds one "
+                                 "of the device's resident segment slots per segment for the segment's lifetime "
+                                 "(lag = S: segment b of every scenario runs after segment b-1's phase), busy with "
+                                 "exact checks / prescans for busy_share of it",
+                      "model_ms_diag": S * sum(life) / slots / (clk * 1e6)})
+        else:
+            launch_cycles = kms * 1e-3 * clk * 1e9
+            m.update({"segments": g["B"], "stages": g["B"] * g["W"],
+                      "stages_busy_on_average": busy / launch_cycles,
+                      "note": "one scenario: every container walks the one-group stages in FFD order until a node fits "
+                              "(visits per container = container_stage_visits / C); the summed busy cycles over the "
+                              "launch's cycles give the stages busy at once -- the chain of exact checks at the "
+                              "placement frontier sets the time, not memory"})
+        latest[leg] = m
+        print(leg, json.dumps(m), flush=True)
     with open(out_path, "w") as fo:
-        json.dump(res, fo, indent=1)
+        json.dump(latest, fo, indent=1)
+    with open(out_path.replace(".json", "_raw.json"), "w") as fo:
+        json.dump(raw, fo, indent=1)
 
 
 if __name__ == "__main__":
