@@ -16,7 +16,21 @@
 #pragma once
 #include <stdint.h>
 
+// re-test of a group's queue after its first miss (fpp_group_x), with a batch corner of at
+// most FP_REFILTER_MAX nodes; -DFP_REFILTER=0 for A/B runs
+#ifndef FP_REFILTER
+#define FP_REFILTER 1
+#endif
+#ifndef FP_REFILTER_MAX
+#define FP_REFILTER_MAX 16
+#endif
+
 namespace fpp {
+
+__device__ __forceinline__ uint64_t fpp_uniform64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
 
 typedef uint32_t rec10 __attribute__((ext_vector_type(10)));
 
@@ -155,7 +169,7 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
                                               uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
                                               uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
                                               uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
-                                              uint32_t &nhit) {
+                                              uint32_t &nhit, uint32_t, uint32_t) {
     constexpr uint32_t nmask = g < 32 ? ~((2u << g) - 1u) : 0u;        // candidate groups above g
     constexpr uint32_t nmask_hi = g < 32 ? 0xFFFFFFFFu : ~((2u << (g & 31)) - 1u);
     constexpr uint32_t goff = g * 64u;
@@ -247,53 +261,71 @@ __device__ __forceinline__ void fpp_asm_group(uint64_t q, uint64_t &placed, uint
 //     (0xFFFFFFFF) on a miss (l = -1).  The caller derives `placed` and the next candidate
 //     group of the misses from asg once per group (vector ops off the chain).
 // touched |= the nodes placed on (for the deferred mask / used-bit bookkeeping).
-__device__ __forceinline__ void fpp_asm_group_x(uint64_t q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
+// STOP: leave the loop after the first miss, with q = the containers not yet checked (the
+// caller re-filters them against the group's current state); else run q to the end.  The two
+// bodies differ in one line (qx = miss ? 0 : q) and in the register the loop test reads.
+#define FPP_GX_BODY(SEL, TEST)                                                              \
+    "s_cmp_eq_u64 %[q], 0\n\t"                                                             \
+    "s_cbranch_scc1 .Lfgx_end%=\n\t"                                                       \
+    "s_mov_b64 %[esv], exec\n"                                                             \
+    ".Lfgx_loop%=:\n\t"                                                                    \
+    "s_ff1_i32_b64 %[t], %[q]\n\t"                                                         \
+    "v_readlane_b32 %[kc], %[cpu], %[t]\n\t"                                               \
+    "v_readlane_b32 %[km], %[mem], %[t]\n\t"                                               \
+    "v_readlane_b32 %[kr], %[req], %[t]\n\t"                                               \
+    "v_readlane_b32 %[kx], %[conf], %[t]\n\t"                                              \
+    "s_bitset0_b64 %[q], %[t]\n\t"                                                         \
+    FPP_ASM_CNT_CHECK                                                                      \
+    "v_cmp_ge_u32_e64 %[m1], %[rcf], %[kc]\n\t"                                            \
+    "v_cmp_ge_u32_e64 %[m2], %[rmf], %[km]\n\t"                                            \
+    "v_and_b32_e32 %[t0], %[kr], %[rlab]\n\t"                                              \
+    "v_and_or_b32 %[t0], %[rcu], %[kx], %[t0]\n\t"                                         \
+    "v_cmp_eq_u32_e64 %[m3], 0, %[t0]\n\t"                                                 \
+    "s_and_b64 %[m1], %[m1], %[m2]\n\t"                                                    \
+    "s_and_b64 %[m1], %[m1], %[m3]\n\t"                                                    \
+    SEL                                                                                    \
+    "s_ff1_i32_b64 %[l], %[m1]\n\t"                                                        \
+    "s_lshl_b64 %[m2], 1, %[l]\n\t"                                                        \
+    "s_and_b64 exec, %[m2], %[m1]\n\t"        /* {l}, or {} on a miss */                   \
+    "v_subrev_u32_e32 %[rcf], %[kc], %[rcf]\n\t"                                           \
+    "v_subrev_u32_e32 %[rmf], %[km], %[rmf]\n\t"                                           \
+    "v_or_b32_e32 %[rcu], %[kx], %[rcu]\n\t"                                               \
+    "s_or_b64 %[touched], %[touched], exec\n\t"                                            \
+    "s_or_b32 %[nv], %[gbg], %[l]\n\t"         /* FP_NONE on a miss */                     \
+    "s_lshl_b64 exec, 1, %[t]\n\t"                                                         \
+    "v_mov_b32_e32 %[asg], %[nv]\n\t"                                                      \
+    "s_mov_b64 exec, %[esv]\n\t"                                                           \
+    "s_cmp_lg_u64 " TEST ", 0\n\t"                                                         \
+    "s_cbranch_scc1 .Lfgx_loop%=\n"                                                        \
+    ".Lfgx_end%=:"
+#define FPP_GX_OPERANDS                                                                                         \
+    : [q] "+s"(q), [touched] "+s"(touched), [asg] "+v"(asg), [rcf] "+v"(rcf), [rmf] "+v"(rmf), [rcu] "+v"(rcu), \
+      [nchk] "+s"(nchk), [t] "=&s"(t), [kc] "=&s"(kc), [km] "=&s"(km), [kr] "=&s"(kr), [kx] "=&s"(kx),          \
+      [l] "=&s"(l), [nv] "=&s"(nv), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [esv] "=&s"(esv),           \
+      [qx] "=&s"(qx), [t0] "=&v"(t0)                                                                            \
+    : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [gbg] "s"(gbg)       \
+    : "scc", "memory"
+template <bool STOP>
+__device__ __forceinline__ void fpp_asm_group_x(uint64_t &q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
                                                 uint32_t &rmf, uint32_t &rcu, uint32_t rlab, uint32_t cpu,
                                                 uint32_t mem, uint32_t req, uint32_t conf, uint32_t gbg,
                                                 uint32_t &nchk) {
     uint32_t t, kc, km, kr, kx, l, nv;
-    uint64_t m1, m2, m3, esv;
+    uint64_t m1, m2, m3, esv, qx;
     uint32_t t0;
-    asm volatile(
-        "s_cmp_eq_u64 %[q], 0\n\t"
-        "s_cbranch_scc1 .Lfgx_end%=\n\t"
-        "s_mov_b64 %[esv], exec\n"
-        ".Lfgx_loop%=:\n\t"
-        "s_ff1_i32_b64 %[t], %[q]\n\t"
-        "v_readlane_b32 %[kc], %[cpu], %[t]\n\t"
-        "v_readlane_b32 %[km], %[mem], %[t]\n\t"
-        "v_readlane_b32 %[kr], %[req], %[t]\n\t"
-        "v_readlane_b32 %[kx], %[conf], %[t]\n\t"
-        "s_bitset0_b64 %[q], %[t]\n\t"
-        FPP_ASM_CNT_CHECK
-        "v_cmp_ge_u32_e64 %[m1], %[rcf], %[kc]\n\t"
-        "v_cmp_ge_u32_e64 %[m2], %[rmf], %[km]\n\t"
-        "v_and_b32_e32 %[t0], %[kr], %[rlab]\n\t"
-        "v_and_or_b32 %[t0], %[rcu], %[kx], %[t0]\n\t"
-        "v_cmp_eq_u32_e64 %[m3], 0, %[t0]\n\t"
-        "s_and_b64 %[m1], %[m1], %[m2]\n\t"
-        "s_and_b64 %[m1], %[m1], %[m3]\n\t"
-        "s_ff1_i32_b64 %[l], %[m1]\n\t"
-        "s_lshl_b64 %[m2], 1, %[l]\n\t"
-        "s_and_b64 exec, %[m2], %[m1]\n\t"        // {l}, or {} on a miss
-        "v_subrev_u32_e32 %[rcf], %[kc], %[rcf]\n\t"
-        "v_subrev_u32_e32 %[rmf], %[km], %[rmf]\n\t"
-        "v_or_b32_e32 %[rcu], %[kx], %[rcu]\n\t"
-        "s_or_b64 %[touched], %[touched], exec\n\t"
-        "s_or_b32 %[nv], %[gbg], %[l]\n\t"         // FP_NONE on a miss
-        "s_lshl_b64 exec, 1, %[t]\n\t"
-        "v_mov_b32_e32 %[asg], %[nv]\n\t"
-        "s_mov_b64 exec, %[esv]\n\t"
-        "s_cmp_lg_u64 %[q], 0\n\t"
-        "s_cbranch_scc1 .Lfgx_loop%=\n"
-        ".Lfgx_end%=:"
-        : [q] "+s"(q), [touched] "+s"(touched), [asg] "+v"(asg), [rcf] "+v"(rcf), [rmf] "+v"(rmf), [rcu] "+v"(rcu),
-          [nchk] "+s"(nchk), [t] "=&s"(t), [kc] "=&s"(kc), [km] "=&s"(km), [kr] "=&s"(kr), [kx] "=&s"(kx),
-          [l] "=&s"(l), [nv] "=&s"(nv), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [esv] "=&s"(esv),
-          [t0] "=&v"(t0)
-        : [rlab] "v"(rlab), [cpu] "v"(cpu), [mem] "v"(mem), [req] "v"(req), [conf] "v"(conf), [gbg] "s"(gbg)
-        : "scc", "memory");
+    if constexpr (STOP)
+        asm volatile(FPP_GX_BODY("s_cselect_b64 %[qx], %[q], 0\n\t", "%[qx]") FPP_GX_OPERANDS);
+    else
+        asm volatile(FPP_GX_BODY("", "%[q]") FPP_GX_OPERANDS);
+    (void)qx;
+    // the asm's scalar outputs are wave-uniform, which divergence analysis cannot see: say so,
+    // so that they can feed the next call's "+s" operands inside the caller's loop
+    q = fpp_uniform64(q);
+    touched = fpp_uniform64(touched);
+    nchk = (uint32_t)__builtin_amdgcn_readfirstlane((int)nchk);
 }
+#undef FPP_GX_BODY
+#undef FPP_GX_OPERANDS
 
 // Drop-in for fpp_asm_group (same arguments): the exec-masked loop plus the per-group
 // vector epilogue -- placed bits of the hits, next candidate group of the misses.
@@ -302,8 +334,46 @@ __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64
                                             uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
                                             uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
                                             uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
-                                            uint32_t &nhit) {
-    fpp_asm_group_x(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+                                            uint32_t &nhit, uint32_t qc, uint32_t qm) {
+    const uint64_t q0 = q;
+#if FP_REFILTER
+    // Stop at the first miss and re-test the rest of the queue, vector-parallel, against the
+    // group's current state: a miss usually means the group just filled up for the batch's
+    // sizes, so the containers behind it fail too (failed checks: 33 k of 71 k per config-4
+    // scenario, 1.2 M of 1.96 M in config 3; almost none are visible at the queue's start).
+    // The test is exact: the nodes of the batch corner (every node that could take the batch's
+    // smallest demands) are broadcast and each queued lane tests its own container; one that
+    // fits none of them now never will (monotone).  A large corner, or a re-test that drops
+    // nothing, finishes the queue in the plain loop.
+    fpp_asm_group_x<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+    while (q) {
+        uint64_t e = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
+        uint64_t fit = 0;
+        if (__builtin_popcountll(e) <= FP_REFILTER_MAX) {
+            bool ok = false;
+            while (e) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(e);
+                e &= e - 1;
+                const uint32_t ncf = __builtin_amdgcn_readlane(rcf, l), nmf = __builtin_amdgcn_readlane(rmf, l);
+                const uint32_t nlb = __builtin_amdgcn_readlane(rlab, l), ncu = __builtin_amdgcn_readlane(rcu, l);
+                ok |= (ncf >= cpu) & (nmf >= mem) & (((req & nlb) | (conf & ncu)) == 0u);
+            }
+            fit = q & __builtin_amdgcn_ballot_w64(ok);
+        } else {
+            fit = q;
+        }
+        if (fit == q) {  // nothing to drop: the rest of the queue in the plain loop
+            fpp_asm_group_x<false>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+            break;
+        }
+        q = fit;  // the dropped lanes keep asg = FP_NONE: misses of this group
+        fpp_asm_group_x<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+    }
+#else
+    (void)qc; (void)qm;
+    fpp_asm_group_x<false>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+#endif
+    q = q0;
     const uint32_t lane = __lane_id();
     const bool inq = (q >> lane) & 1ull;
     const uint64_t hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);

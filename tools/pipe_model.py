@@ -96,7 +96,8 @@ def main():
                     "per_stage_slot": [{"visits": r[0] / S, "checks": r[1] / S, "hits": r[2] / S, "batches": r[3] / S,
                                         "input_Mcycles": r[8] / S / 1e6, "prescan_Mcycles": r[9] / S / 1e6,
                                         "cand_Mcycles": r[10] / S / 1e6, "fwd_Mcycles": r[11] / S / 1e6,
-                                        "out_wait_Mcycles": r[12] / S / 1e6, "life_Mcycles": r[13] / S / 1e6}
+                                        "out_wait_Mcycles": r[12] / S / 1e6, "life_Mcycles": r[13] / S / 1e6,
+                                        "queued_fit_no_node_at_queue_start": r[6] / S}
                                        for r in v]}
         m = {"C": C, "N": N, "S_diag": S, "source": "tools/pipe_model.py, diagnostics build (libfleetplace_stats.so)",
              "geometry": g, "clock_ghz": clk, "kernel_ms_diag_build": kms,
