@@ -192,6 +192,8 @@ def roofline(leg, S, C, N, kernel_s, step_s):
         lm = dict(m, measured_kernel_ms=kernel_s * 1e3)
         if "slot_cycles_per_scenario" in m:
             lm["model_ms"] = S * m["slot_cycles_per_scenario"] / m["slots"] / (m["clock_ghz"] * 1e6)
+        elif "front" in m:
+            lm["model_ms"] = m["front"]["model_ms"]
         if traffic:
             lm["hbm_time_at_peak_ms"] = traffic / (HBM_PEAK_GBPS * 1e9) * 1e3
         out["latency_model"] = lm

@@ -258,7 +258,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
-                                           uint32_t &nhit, uint32_t &ncatch) {
+                                           uint32_t &nhit) {
     (
         [&] {
             uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
@@ -283,17 +283,6 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                     }
                     q = fit;
                 }
-            }
-            if (STAT_ON && q) {
-                // diagnostics: queued containers that fit no node of the group by capacity at the
-                // queue's start (an exact filter could drop them before the serial loop)
-                bool anyfit = false;
-                for (uint32_t l = 0; l < 64; ++l) {
-                    const uint32_t ncf = __builtin_amdgcn_readlane(rcf[gs], l);
-                    const uint32_t nmf = __builtin_amdgcn_readlane(rmf[gs], l);
-                    anyfit |= (ncf >= cpu) & (nmf >= mem);
-                }
-                ncatch += (uint32_t)__popcll(q & __builtin_amdgcn_ballot_w64(!anyfit));
             }
             if (q) {
                 uint64_t touched = 0;
@@ -755,7 +744,7 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe
             fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                    used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                    (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
-                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, st_miss[0]);
+                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
 #else
 #pragma unroll

@@ -81,6 +81,33 @@ def measure(p, S, C, N, seed):
     return ms / n, placed, [r for r in v if any(r)]  # counters of the last launch (reset before it)
 
 
+def front_model(p, kms):
+    """Config 3: per-stage spans of scenario 0 (fp_debug_stage_span, filled by the launch that
+    measure() just ran).  The first container reaches stage j at ~ j x front_us_per_stage:
+    stage j - 1 forwards only once its group is full for the stream's current sizes, and it
+    fills its group by serial exact checks -- so the launch is the time for that front to
+    cross every stage plus the last stages' drain."""
+    L = _lib.load()
+    f = L.fp_debug_stage_span
+    f.argtypes = [ct.POINTER(ct.c_ulonglong)]
+    buf = (ct.c_ulonglong * (4096 * 8))()
+    f(buf)
+    rows = [[buf[i * 8 + k] for k in range(8)] for i in range(4096)]
+    rows = [r for r in rows if r[0]]
+    t0 = min(r[0] for r in rows)
+    first = [(r[1] - t0) / 100.0 for r in rows]  # us (s_memrealtime, 100 MHz)
+    end = [(r[2] - t0) / 100.0 for r in rows]
+    n = len(rows)
+    lo, hi = n // 10, n - 1  # slope of the front past the start-up
+    slope = (first[hi] - first[lo]) / (hi - lo)
+    return {"stages_traced": n, "front_us_per_stage": slope, "first_input_last_stage_us": first[-1],
+            "last_stage_drain_us": end[-1] - first[-1], "launch_end_us": max(end),
+            "model_ms": (slope * n + (end[-1] - first[-1])) / 1e3, "placements_per_stage": sum(r[7] for r in rows) / n,
+            "formula": "kernel_ms ~ front_us_per_stage x stages + last-stage drain: stage j - 1 forwards its first "
+                       "container once its group is full for the stream's sizes, so the groups fill one after another "
+                       "by serial exact checks (~175 cycles each) -- the launch is bound by that front, not by memory"}
+
+
 def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pipe_model.json")
     p = Planner(0)
@@ -96,8 +123,7 @@ def main():
                     "per_stage_slot": [{"visits": r[0] / S, "checks": r[1] / S, "hits": r[2] / S, "batches": r[3] / S,
                                         "input_Mcycles": r[8] / S / 1e6, "prescan_Mcycles": r[9] / S / 1e6,
                                         "cand_Mcycles": r[10] / S / 1e6, "fwd_Mcycles": r[11] / S / 1e6,
-                                        "out_wait_Mcycles": r[12] / S / 1e6, "life_Mcycles": r[13] / S / 1e6,
-                                        "queued_fit_no_node_at_queue_start": r[6] / S}
+                                        "out_wait_Mcycles": r[12] / S / 1e6, "life_Mcycles": r[13] / S / 1e6}
                                        for r in v]}
         m = {"C": C, "N": N, "S_diag": S, "source": "tools/pipe_model.py, diagnostics build (libfleetplace_stats.so)",
              "geometry": g, "clock_ghz": clk, "kernel_ms_diag_build": kms,
@@ -115,6 +141,7 @@ def main():
                                  "exact checks / prescans for busy_share of it",
                       "model_ms_diag": S * sum(life) / slots / (clk * 1e6)})
         else:
+            m["front"] = front_model(p, kms)
             launch_cycles = kms * 1e-3 * clk * 1e9
             m.update({"segments": g["B"], "stages": g["B"] * g["W"],
                       "stages_busy_on_average": busy / launch_cycles,
