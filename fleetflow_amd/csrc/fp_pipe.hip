@@ -321,8 +321,16 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
 #ifndef FP_WIDE_WAVES
 #define FP_WIDE_WAVES 3
 #endif
+// One-wave segments of 12 groups (many-scenario batches) are compiled as 64-thread kernels for
+// FP_WIDE12_WAVES waves per SIMD: 5 fits them in 96 VGPRs (32 B of scratch) and 20 segments per
+// CU -- config-4 FFD 20.9 -> 18.7 ms against the 1024-thread kernel's 107 VGPRs and four waves
+// (6 waves: 80 VGPRs, 100 B of scratch, 19.2 ms).  0 selects the 1024-thread kernel.
+#ifndef FP_WIDE12_WAVES
+#define FP_WIDE12_WAVES 5
+#endif
 template <uint32_t G, uint32_t BLK>
-__global__ __launch_bounds__(BLK, BLK == 64 ? FP_WIDE_WAVES : 1) void k_ffd_pipe(const PipeArgs a) {
+__global__ __launch_bounds__(BLK, BLK == 64 ? (G == 12 && FP_WIDE12_WAVES ? FP_WIDE12_WAVES : FP_WIDE_WAVES) : 1) void
+k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = a.W, R = a.R, B = a.B;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1222,13 +1230,14 @@ static const launch_fn kLaunch[MAX_G + 1] = {
 constexpr uint32_t MAX_G_WIDE = 40;
 #ifndef FP_LEGACY_LOOP
 static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {
-    nullptr, nullptr, nullptr, nullptr, launch_g<16, 64>, launch_g<20, 64>,
+    nullptr, nullptr, nullptr, FP_WIDE12_WAVES ? launch_g<12, 64> : nullptr, launch_g<16, 64>, launch_g<20, 64>,
     launch_g<24, 64>, launch_g<28, 64>, launch_g<32, 64>, launch_g<36, 64>, launch_g<40, 64>};
 static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {
-    nullptr, nullptr, nullptr, nullptr, (const void *)k_ffd_pipe<16, 64>, (const void *)k_ffd_pipe<20, 64>,
+    nullptr, nullptr, nullptr, FP_WIDE12_WAVES ? (const void *)k_ffd_pipe<12, 64> : nullptr,
+    (const void *)k_ffd_pipe<16, 64>, (const void *)k_ffd_pipe<20, 64>,
     (const void *)k_ffd_pipe<24, 64>, (const void *)k_ffd_pipe<28, 64>, (const void *)k_ffd_pipe<32, 64>,
     (const void *)k_ffd_pipe<36, 64>, (const void *)k_ffd_pipe<40, 64>};
-static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G > 12; }
+static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && (G > 12 || (FP_WIDE12_WAVES && G == 12)); }
 #else  // round 1's loops take at most 16 groups per stage
 static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {nullptr};
 static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {nullptr};
@@ -1285,8 +1294,8 @@ bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint
     // placement frontier moves through them), so one wave does the same work in about the
     // same time while a scenario needs fewer registers than with 4-stage segments.
     const bool narrow = (uint64_t)S * NG <= kNarrowWaves;
-    // one-wave segments hold at most 12 groups (<= 128 VGPRs, four waves per SIMD, 16
-    // segments in flight per CU).  With lagged segment tickets (the kernel) a segment runs
+    // one-wave segments hold at most 12 groups (96 VGPRs at five waves per SIMD, 20
+    // segments in flight per CU; FP_WIDE12_WAVES).  With lagged segment tickets (the kernel) a segment runs
     // on complete input, so more, smaller segments keep more waves busy: config 4 (79
     // groups) 7 segments of 12 groups 28.3 ms, 10 of 8 groups 28.2, 4 of 20 groups 30.3,
     // 3 of 24-28 groups 30.2.  (Without the lag, when a segment waited on its upstream
