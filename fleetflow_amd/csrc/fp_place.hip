@@ -370,7 +370,9 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     const uint64_t lt = (1ull << lane) - 1ull;
     const size_t cb = (size_t)blockIdx.x * C;
     const uint16_t *dig = a.dig + cb;
-    const uint32_t hbits = 32u - (uint32_t)__builtin_clz(dc | 1u), lbits = 32u - (uint32_t)__builtin_clz(dm | 1u);
+    // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
+    const uint32_t hbits = dc > 1 ? 32u - (uint32_t)__builtin_clz(dc - 1u) : 0u;
+    const uint32_t lbits = dm > 1 ? 32u - (uint32_t)__builtin_clz(dm - 1u) : 0u;
 
     for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
     if (t < SS_DIG) {
