@@ -18,6 +18,13 @@ FP_OK, FP_EINVAL, FP_ENOMEM, FP_EDEVICE, FP_EOVERFLOW, FP_ECORRUPT = 0, -1, -2, 
 FP_NONE = 0xFFFFFFFF
 REASON_OK, REASON_NOFIT, REASON_CYCLE = 0, 1, 2
 FP_K_PLACE, FP_K_SORT, FP_K_FEAS, FP_K_LEVEL, FP_K_GEN = 0, 1, 2, 3, 4
+# context options (fleetplace.h enum fp_option); FP_OPT_AUTO = the production default
+FP_OPT_AUTO = -1
+OPTIONS = {"pipe_w": 0, "pipe_seg": 1, "pipe_r": 2, "pipe_lag": 3, "link_slots": 4, "link_bounded": 5,
+           "pipe_flush": 6, "spin_ticks": 7, "kpack": 8, "scen_sort": 9, "segsort": 10, "systolic": 11,
+           "levelize_sync": 12}
+# fp_place_geometry out[] (fleetplace.h FP_GEOM_*)
+GEOM_FIELDS = ("groups", "stages", "segments", "ring", "lag", "link_slots", "bounded", "resident", "systolic")
 
 u8p = ct.POINTER(ct.c_uint8)
 u32p = ct.POINTER(ct.c_uint32)
@@ -67,6 +74,8 @@ SIGNATURES = {
     "fp_abi_version": (ct.c_int, []),
     "fp_ctx_profile": (ct.c_int, [vp, ct.c_int]),
     "fp_ctx_kernel_stats": (ct.c_int, [vp, ct.c_int, ct.POINTER(ct.c_double), ct.POINTER(ct.c_uint64)]),
+    "fp_ctx_set_option": (ct.c_int, [vp, ct.c_int, ct.c_int64]),
+    "fp_ctx_get_option": (ct.c_int, [vp, ct.c_int, ct.POINTER(ct.c_int64)]),
     "fp_legacy_order": (ct.c_int, [vp, ct.POINTER(FpGraph), u32p]),
     "fp_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), u32p, u32p, u32p]),
     "fp_place": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p, u8p]),
@@ -76,6 +85,7 @@ SIGNATURES = {
     "fp_dev_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), vp, vp, vp]),
     "fp_dev_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),
     "fp_place_ws_bytes": (ct.c_int, [vp, ct.c_uint32, ct.c_uint32, ct.c_uint32, u64p]),
+    "fp_place_geometry": (ct.c_int, [vp, ct.c_uint32, ct.c_uint32, ct.c_uint32, u32p]),
     "fp_dev_feasibility": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), vp, vp, vp]),
     "fp_dev_feasibility_batch": (ct.c_int, [vp, ct.POINTER(FpBatch), vp, vp]),
     "fp_dev_argmin_cost": (ct.c_int, [vp, vp, ct.c_uint32, vp]),

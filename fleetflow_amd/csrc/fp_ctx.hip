@@ -39,17 +39,20 @@ extern "C" int fp_ctx_create(fp_ctx **out, int device) {
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FP_EDEVICE;
     fp_ctx *c = new fp_ctx();
     c->device = device;
+    for (int k = 0; k < FP_OPT_COUNT; ++k) c->opt[k] = FP_OPT_AUTO;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->d_err, 256) != hipSuccess ||
+        hipMalloc(&c->d_err_base, 256) != hipSuccess ||
+        hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&c->h_small, 4096, hipHostMallocDefault) != hipSuccess) {
         fp_ctx_destroy(c);
         return FP_EDEVICE;
     }
-    if (hipMemset(c->d_err, 0, 256) != hipSuccess) {
+    if (hipMemset(c->d_err_base, 0, 256) != hipSuccess) {
         fp_ctx_destroy(c);
         return FP_EDEVICE;
     }
+    c->d_err = c->d_err_base;
     c->stream = c->own_stream;
     *out = c;
     return FP_OK;
@@ -58,27 +61,42 @@ extern "C" int fp_ctx_create(fp_ctx **out, int device) {
 extern "C" void fp_ctx_destroy(fp_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->last_ev) (void)hipEventSynchronize(c->last_ev);
     for (auto &r : c->pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
     if (c->ws) (void)hipFree(c->ws);
     if (c->stage) (void)hipFree(c->stage);
-    if (c->d_err) (void)hipFree(c->d_err);
+    if (c->d_err_base) (void)hipFree(c->d_err_base);
+    if (c->last_ev) (void)hipEventDestroy(c->last_ev);
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
 
-// Switching streams drains the old one first: the workspace arena is reset by every call,
-// so work still queued on the old stream must not overlap a call on the new one.
+// Switching streams first waits for this context's work on the old one: the workspace arena
+// is reset by every call, so it must not overlap a call on the new stream.  It waits on the
+// event the last fp_dev_* call recorded, never on the old stream handle itself, which the
+// caller may already have destroyed.
 extern "C" int fp_ctx_set_stream(fp_ctx *c, void *s) {
     if (!c) return FP_EINVAL;
     if ((hipStream_t)s != c->stream) {
         FP_HIP(hipSetDevice(c->device));
-        FP_HIP(hipStreamSynchronize(c->stream));
+        FP_HIP(hipEventSynchronize(c->last_ev));
     }
     c->stream = (hipStream_t)s;  // NULL = HIP null stream
+    return FP_OK;
+}
+
+extern "C" int fp_ctx_set_option(fp_ctx *c, int k, int64_t v) {
+    if (!c || k < 0 || k >= FP_OPT_COUNT || v < FP_OPT_AUTO) return FP_EINVAL;
+    c->opt[k] = v;
+    return FP_OK;
+}
+
+extern "C" int fp_ctx_get_option(fp_ctx *c, int k, int64_t *v) {
+    if (!c || !v || k < 0 || k >= FP_OPT_COUNT) return FP_EINVAL;
+    *v = c->opt[k];
     return FP_OK;
 }
 
@@ -91,7 +109,14 @@ extern "C" int fp_ctx_reset_stream(fp_ctx *c) {
 extern "C" int fp_ctx_sync(fp_ctx *c) {
     if (!c) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
+    c->d_err = c->d_err_base;
     return fp_take_err(c);
+}
+
+// the end of every fp_dev_* entry point: remember where this context's work ends
+static int dev_done(fp_ctx *c, int rc) {
+    if (hipEventRecord(c->last_ev, c->stream) != hipSuccess && rc == FP_OK) rc = FP_EDEVICE;
+    return rc;
 }
 
 // ---- arenas ----------------------------------------------------------------
@@ -195,18 +220,18 @@ extern "C" int fp_ctx_kernel_stats(fp_ctx *c, int kid, double *total_ms, uint64_
 extern "C" int fp_dev_place_batch(fp_ctx *c, const fp_batch *b) {
     if (!c || !b) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return fp_dev_place_batch_impl(c, b);
+    return dev_done(c, fp_dev_place_batch_impl(c, b));
 }
 extern "C" int fp_dev_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t *order,
                                uint32_t *n_cycle_dev) {
     if (!c || !g) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return fp_dev_levelize_impl(c, g, level, order, n_cycle_dev);
+    return dev_done(c, fp_dev_levelize_impl(c, g, level, order, n_cycle_dev));
 }
 extern "C" int fp_dev_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
     if (!c || !g) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return fp_dev_legacy_order_impl(c, g, perm);
+    return dev_done(c, fp_dev_legacy_order_impl(c, g, perm));
 }
 extern "C" int fp_place_ws_bytes(fp_ctx *c, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes,
                                  uint64_t *bytes_out) {
@@ -214,16 +239,22 @@ extern "C" int fp_place_ws_bytes(fp_ctx *c, uint32_t n_scen, uint32_t n_containe
     FP_HIP(hipSetDevice(c->device));
     return fp_place_ws_bytes_impl(c, n_scen, n_containers, n_nodes, bytes_out);
 }
+extern "C" int fp_place_geometry(fp_ctx *c, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes,
+                                 uint32_t *out) {
+    if (!c || !out) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_place_geometry_impl(c, n_scen, n_containers, n_nodes, out);
+}
 extern "C" int fp_dev_feasibility_batch(fp_ctx *c, const fp_batch *b, uint32_t *first, uint32_t *count) {
     if (!c || !b) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return fp_dev_feasibility_batch_impl(c, b, first, count);
+    return dev_done(c, fp_dev_feasibility_batch_impl(c, b, first, count));
 }
 extern "C" int fp_dev_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
                                   uint32_t *first, uint32_t *count, uint64_t *bitmap) {
     if (!c || !cs || !ns) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return fp_dev_feasibility_impl(c, cs, ns, first, count, bitmap);
+    return dev_done(c, fp_dev_feasibility_impl(c, cs, ns, first, count, bitmap));
 }
 
 // ---- host-pointer entry points -------------------------------------------------
@@ -283,6 +314,7 @@ static int copy_back_all(fp_ctx *c, const OutCopy *o, int n) {
 
 extern "C" int fp_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm_out) {
     if (!c || !g || (g->n_vertices && (!g->has_deps || !perm_out))) return FP_EINVAL;
+    fp_host_err_scope es(c);
     FP_HIP(hipSetDevice(c->device));
     const size_t V = g->n_vertices;
     int rc = fp_stage_reserve(c, 2 * V * 4 + 4096);
@@ -313,6 +345,7 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
     }
     // the CSR is validated on the device (k_check_csr, k_indeg): FP_ECORRUPT
     FP_HIP(hipSetDevice(c->device));
+    fp_host_err_scope es(c);
     int rc = fp_stage_reserve(c, (V + 1) * 4 + E * 4 + V + 2 * V * 4 + 8 * 256);
     if (rc) return rc;
     fp_stage_reset(c);
@@ -331,6 +364,7 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
 }
 
 static int batch_host(fp_ctx *c, const fp_batch *b) {
+    fp_host_err_scope es(c);
     const size_t S = b->n_scen, C = b->n_containers, N = b->n_nodes;
     const size_t SC = S * C, SN = S * N;
     if (S && C && (!b->cpu_m || !b->mem_mib || !b->req_labels || !b->conflict || !b->assign ||
@@ -407,6 +441,7 @@ extern "C" int fp_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes
               !ns->schedulable))
         return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
+    fp_host_err_scope es(c);
     int rc = fp_stage_reserve(c, C * 24 + N * 17 + (bitmap_out ? WC * N * 8 : 0) + 16 * 256);
     if (rc) return rc;
     fp_stage_reset(c);

@@ -18,11 +18,20 @@ struct fp_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    // kernel-side error word (a CSR index out of range, the pipeline's deadlock guard):
-    // sticky -- kernels atomicMax into it, and only fp_take_err (fp_ctx_sync, the end of
-    // every host-pointer call, the levelizer's mid-call checks) reads and clears it, so an
-    // asynchronous call's error survives later calls until someone reports it
+    // kernel-side error words (a CSR index out of range, the pipeline's deadlock guard):
+    // kernels atomicMax into the CURRENT word `d_err`.  fp_dev_* calls use the async word
+    // (d_err_base[0]): sticky until fp_ctx_sync reports and clears it.  A host-pointer call
+    // switches to its own word (d_err_base[HOST_ERR]) for its duration and reports only that
+    // one, so an earlier async failure neither fails an unrelated synchronous call nor gets
+    // cleared by it
+    static constexpr uint32_t HOST_ERR = 32;
+    uint32_t *d_err_base = nullptr;
     uint32_t *d_err = nullptr;
+    // per-context options (fp_ctx_set_option; FP_OPT_AUTO = production default)
+    int64_t opt[FP_OPT_COUNT];
+    // recorded on the launch stream at the end of every fp_dev_* call: fp_ctx_set_stream
+    // waits on it instead of synchronising a stream handle the caller may have destroyed
+    hipEvent_t last_ev = nullptr;
     // device workspace: a bump arena reset at the start of every API call
     char *ws = nullptr;
     size_t ws_cap = 0, ws_top = 0;
@@ -56,8 +65,20 @@ void *fp_stage_take(fp_ctx *c, size_t bytes);
 void fp_prof_begin(fp_ctx *c, int kid, hipEvent_t *a);
 void fp_prof_end(fp_ctx *c, int kid, hipEvent_t a);
 
-// synchronise the stream, read the sticky kernel error word and clear it (0 or -FP_E*)
+// synchronise the stream, read the current kernel error word and clear it (0 or -FP_E*)
 int fp_take_err(fp_ctx *c);
+
+// option value, or `dflt` when the option is FP_OPT_AUTO
+static inline int64_t fp_opt(const fp_ctx *c, int k, int64_t dflt) {
+    return (c && c->opt[k] != FP_OPT_AUTO) ? c->opt[k] : dflt;
+}
+
+// a host-pointer call's own kernel error word for its duration (fp_internal.h fp_ctx)
+struct fp_host_err_scope {
+    fp_ctx *c;
+    explicit fp_host_err_scope(fp_ctx *cc) : c(cc) { c->d_err = c->d_err_base + fp_ctx::HOST_ERR; }
+    ~fp_host_err_scope() { c->d_err = c->d_err_base; }
+};
 
 static inline uint32_t fp_bitwidth(uint64_t v) {
     uint32_t b = 0;
@@ -75,7 +96,9 @@ int fp_dev_feasibility_impl(fp_ctx *c, const fp_containers *cs, const fp_nodes *
 int fp_dev_feasibility_batch_impl(fp_ctx *c, const fp_batch *b, uint32_t *first, uint32_t *count);
 
 // tile-pipeline FFD (fp_pipe.hip)
-bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out);
+bool fp_pipe_plan(const fp_ctx *c, uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out,
+                  size_t *lds_out);
+int fp_place_geometry_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t *out);
 size_t fp_pipe_ws_bytes(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N);
 int fp_place_ws_bytes_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint64_t *bytes);
 // bucket thresholds of the candidate masks: K ascending values, T[0] = 0
@@ -87,7 +110,7 @@ struct fp_pipe_soa {
 };
 int fp_pipe_soa_take(fp_ctx *c, size_t SC, fp_pipe_soa *soa);
 // 1 when the position word carries the bucket indices (bits 21-30)
-uint32_t fp_pipe_kpack(uint32_t C);
+uint32_t fp_pipe_kpack(const fp_ctx *c, uint32_t C);
 // ready: the per-scenario LDS sort already wrote order, s_cpu, s_mem and s_idx (only the
 // req / conf / CYCLE gather remains); null: gather everything from order + sorted keys
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,

@@ -5,7 +5,7 @@
 //    computed with wavefront ballots + a block-offset scan.
 //  * fp_dev_levelize: SPEC.md 2.2, Kahn over the reversed CSR, asynchronous by default
 //    (k_lvl_async: a persistent grid on sharded work queues, no per-level launch;
-//    DESIGN.md 4.4), level-synchronous with FLEETPLACE_LEVELIZE=levels (one k_expand
+//    DESIGN.md 4.4), level-synchronous with FP_OPT_LEVELIZE_SYNC (one k_expand
 //    launch per level).  level(v) = max(has_deps(v), max_{d->v} level(d)+1) is unique,
 //    so neither schedule (nor the atomic order inside it) can change the result.
 #include "fp_internal.h"
@@ -564,8 +564,8 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
             g->col, E, V, indeg, c->d_err);
         FP_HIP(hipGetLastError());
     }
-    // FLEETPLACE_LEVELIZE=levels: the level-synchronous schedule (one launch per level)
-    static const bool level_sync = getenv("FLEETPLACE_LEVELIZE") && !strcmp(getenv("FLEETPLACE_LEVELIZE"), "levels");
+    // FP_OPT_LEVELIZE_SYNC = 1: the level-synchronous schedule (one launch per level)
+    const bool level_sync = fp_opt(c, FP_OPT_LEVELIZE_SYNC, 0) != 0;
     if (!level_sync) {
         if ((uint64_t)V + 65536ull * 64 >= 0xFFFFFFFFull) return FP_EOVERFLOW;  // queue heads stay below 2^32
         uint64_t *state = (uint64_t *)fp_ws_take(c, (size_t)V * 8);

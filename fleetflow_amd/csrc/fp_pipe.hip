@@ -31,6 +31,7 @@
 #define FP_ASM
 #endif
 #include "fp_pipe_asm.h"
+#include "fp_pipe_sys.h"
 #include <stdlib.h>
 #include <string.h>
 #include <type_traits>
@@ -68,7 +69,7 @@ constexpr uint32_t CYC = 0x80000000u;
 // Deadlock guard: a wait longer than this (s_memrealtime runs at 100 MHz) aborts the
 // launch with FP_EDEVICE.  Downstream stages legitimately wait for most of a long
 // launch, so the bound is wall-clock time, not an iteration count.
-constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s (FLEETPLACE_SPIN_TICKS overrides: tests)
+constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s (FP_OPT_SPIN_TICKS overrides: tests)
 constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per group)
 #ifndef FP_SPIN_MAX
 #define FP_SPIN_MAX 12              // longest back-off sleep of an idle stage (x 64 cycles)
@@ -85,6 +86,7 @@ struct PipeArgs {
     uint32_t bounded; // 1: links are rings with back-pressure (every segment co-resident, lag 0)
     uint32_t flush;   // idle flushes of partial output slots: bit 0 LDS rings, bit 1 global links (bounded)
     uint32_t kpack;   // 1: s_idx carries the bucket indices (bits 21-25 cpu, 26-30 mem; C <= 2^21)
+    uint32_t sys;     // systolic group fill for queues of >= sys containers (0: serial loop only)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
     uint32_t *ghead;  // [S][B-1] link control, 256 B apart: [0] head, [32] consumer tail
@@ -258,7 +260,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
-                                           uint32_t &nhit) {
+                                           uint32_t &nhit, uint32_t sys) {
     (
         [&] {
             uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
@@ -286,8 +288,13 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
             }
             if (q) {
                 uint64_t touched = 0;
-                FPP_GROUP_LOOP<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
-                                     req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
+                // long queues (a filling group): the systolic loop, else the serial one
+                if (sys && (uint32_t)__builtin_popcountll(q) >= sys)
+                    fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                                         req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
+                else
+                    FPP_GROUP_LOOP<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                                         req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
                 if (touched) {
                     const bool me = (touched >> lane) & 1ull;
                     if (gs < 32) used |= me ? (1u << gs) : 0u;
@@ -752,7 +759,7 @@ k_ffd_pipe(const PipeArgs a) {
             fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                    used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                    (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
-                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit);
+                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
 #else
 #pragma unroll
@@ -1276,17 +1283,18 @@ constexpr size_t LDS_HALF_CU = 80 * 1024;
 // groups): 160 ms with one-group stages vs 181 ms with 10-group stages (hand-scheduled loop).
 constexpr uint64_t kNarrowWaves = 4096;
 
-bool fp_pipe_plan(uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out, size_t *lds_out) {
+bool fp_pipe_plan(const fp_ctx *c, uint32_t S, uint32_t N, uint32_t *G_out, uint32_t *W_out, uint32_t *B_out,
+                  size_t *lds_out) {
     const uint32_t NG = (N + 63) / 64;
     const size_t cap = 160 * 1024;
     if (NG == 0) {
         *G_out = 1; *W_out = 1; *B_out = 1; *lds_out = lds_bytes(1, 1, 2);
         return true;
     }
-    // FLEETPLACE_PIPE_W: force the stage count (tuning experiments and tests)
-    const int forced_w = getenv("FLEETPLACE_PIPE_W") ? atoi(getenv("FLEETPLACE_PIPE_W")) : 0;
-    // FLEETPLACE_PIPE_SEG: groups per segment (tuning experiments and tests)
-    const int forced_seg = getenv("FLEETPLACE_PIPE_SEG") ? atoi(getenv("FLEETPLACE_PIPE_SEG")) : 0;
+    // FP_OPT_PIPE_W / FP_OPT_PIPE_SEG: force the stage count / groups per segment (tuning
+    // experiments and tests)
+    const int forced_w = (int)fp_opt(c, FP_OPT_PIPE_W, 0);
+    const int forced_seg = (int)fp_opt(c, FP_OPT_PIPE_SEG, 0);
     // Few scenarios leave the GPU idle: one group (64 nodes) per stage then shortens the
     // chain -- config 2 (1 x 10k x 1k): 2.39 ms vs 3.02 ms with 10-group stages; config 3
     // (1 x 1M x 100k): 160 ms vs 181 ms.  Many scenarios get one-wave segments of up to 40
@@ -1331,30 +1339,32 @@ struct PipeGeom {
     uint32_t lag;       // segment ticket lag (kernel comment)
     uint32_t slots;     // slots per global link
     uint32_t bounded;   // links are rings with back-pressure
+    uint32_t resident;  // workgroups of this kernel resident on the device at once (0: unknown)
+    uint32_t sys;       // systolic group fill for queues of >= sys containers (0: off)
 };
 
 // Global link ring size when every segment of the launch is co-resident: 256 slots x 64
-// containers in flight per link (128 KB).  FLEETPLACE_LINK_SLOTS overrides (>= 8; tests
-// force small rings to exercise back-pressure).
+// containers in flight per link (128 KB).  FP_OPT_LINK_SLOTS overrides (>= 8; tests force
+// small rings to exercise back-pressure).
 constexpr uint32_t LINK_RING_SLOTS = 256;
 
 static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g) {
-    if (!fp_pipe_plan(S, N, &g->G, &g->W, &g->B, &g->lds)) return false;
+    if (!fp_pipe_plan(c, S, N, &g->G, &g->W, &g->B, &g->lds)) return false;
     const uint32_t G = g->G, W = g->W, B = g->B;
     // deepest ring (2..4 slots) that keeps two workgroups per CU (else one)
     uint32_t R = 2;
     for (uint32_t r = 4; r > 2; --r)
         if (lds_bytes(W, G, r) <= LDS_HALF_CU) { R = r; break; }
-    // FLEETPLACE_PIPE_R: force the ring depth, 2..6 (a link's control block holds 6 slot counts)
-    if (getenv("FLEETPLACE_PIPE_R")) {
-        const int fr = atoi(getenv("FLEETPLACE_PIPE_R"));
+    // FP_OPT_PIPE_R: force the ring depth, 2..6 (a link's control block holds 6 slot counts)
+    {
+        const int64_t fr = fp_opt(c, FP_OPT_PIPE_R, 0);
         if (fr >= 2 && fr <= 6 && lds_bytes(W, G, (uint32_t)fr) <= 160 * 1024) R = (uint32_t)fr;
     }
     g->R = R;
     g->lds = lds_bytes(W, G, R);
     // resident segments on this device (0 if unknown)
     uint64_t slots_total = 0;
-    if (B > 1) {
+    {
         int dev_cu = 0, occ = 0;
         (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
         const bool wide = wide_g(W, G);
@@ -1363,7 +1373,8 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
         if (fn && dev_cu > 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), g->lds) == hipSuccess && occ > 0)
             slots_total = (uint64_t)occ * (uint64_t)dev_cu;
     }
-    const bool fits = slots_total && (uint64_t)S * B <= slots_total;
+    g->resident = (uint32_t)(slots_total < 0xFFFFFFFFull ? slots_total : 0xFFFFFFFFull);
+    const bool fits = B > 1 && slots_total && (uint64_t)S * B <= slots_total;
     // segment lag (kernel comment).  Measured FFD kernel ms (7 segments of 12 groups, 4096
     // resident slots):
     //   S=4096: lag 600 29.0, 1170 27.5, 2340 26.9, 3000 26.5, 4096 26.3
@@ -1373,22 +1384,29 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     // A segment that never waits on its upstream beats overlap between a scenario's
     // segments once the batch holds more segments than the GPU: lag = S runs the segments
     // index by index (phase b starts as phase b-1's tickets drain).  Batches that fit at
-    // once keep lag 0 so all segments run concurrently.  FLEETPLACE_PIPE_LAG overrides.
-    g->lag = (B > 1 && S > 1 && slots_total && !fits) ? S : 0u;
-    if (getenv("FLEETPLACE_PIPE_LAG")) g->lag = (uint32_t)atoi(getenv("FLEETPLACE_PIPE_LAG"));
-    // Global links.  When every segment is resident at once and segments run side by side
-    // (lag 0), a link is a bounded ring: a producer waiting on a full ring waits on a
-    // consumer that is running, so back-pressure cannot deadlock.  Otherwise a consumer may
-    // start only after its producer finished (lag = S phases, or more segments than slots),
-    // so the link holds every container: (C + 63) / 64 + 2 slots.
+    // once keep lag 0 so all segments run concurrently.  FP_OPT_PIPE_LAG overrides.
+    g->lag = (uint32_t)fp_opt(c, FP_OPT_PIPE_LAG, (B > 1 && S > 1 && slots_total && !fits) ? S : 0u);
+    // Global links.  With lag 0 a producer blocked on a full bounded ring waits for its
+    // consumer, the next segment of the same scenario, which took a later ticket.  The
+    // lowest unfinished ticket's scenario always has every remaining segment resident when
+    // this launch holds at least B slots, so its chain drains and back-pressure cannot
+    // deadlock.  Rings are therefore used only when the whole batch fits (S * B slots) and a
+    // scenario's chain fits twice over (2 * B), a margin for other work sharing the device
+    // (fleetplace.h); otherwise a consumer may start only after its producer finished (lag =
+    // S phases, more segments than slots), so the link holds every container:
+    // (C + 63) / 64 + 2 slots.
     const uint32_t full = (C + 63) / 64 + 2;
     uint32_t ring = LINK_RING_SLOTS;
-    if (getenv("FLEETPLACE_LINK_SLOTS")) {
-        const int v = atoi(getenv("FLEETPLACE_LINK_SLOTS"));
-        if (v >= 8) ring = (uint32_t)v;
+    {
+        const int64_t v = fp_opt(c, FP_OPT_LINK_SLOTS, 0);
+        if (v >= 8 && v < (int64_t)full) ring = (uint32_t)v;
     }
-    g->bounded = (fits && g->lag == 0 && ring < full) ? 1u : 0u;
-    g->slots = g->bounded ? ring : full;
+    const bool margin = 2ull * B <= slots_total;
+    g->bounded = (uint32_t)fp_opt(c, FP_OPT_LINK_BOUNDED, (fits && margin && g->lag == 0 && ring < full) ? 1 : 0);
+    if (B <= 1) g->bounded = 0;
+    g->slots = g->bounded ? (ring < full ? ring : full) : full;
+    // systolic group fill (fp_pipe_sys.h): queues of at least this many containers
+    g->sys = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 0);
     return true;
 }
 
@@ -1401,8 +1419,8 @@ size_t fp_pipe_ws_bytes(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N) {
            10 * 256;
 }
 
-uint32_t fp_pipe_kpack(uint32_t C) {
-    return C <= (IDX_POS_MASK + 1u) && !(getenv("FLEETPLACE_NO_KPACK") && atoi(getenv("FLEETPLACE_NO_KPACK")));
+uint32_t fp_pipe_kpack(const fp_ctx *c, uint32_t C) {
+    return C <= (IDX_POS_MASK + 1u) && fp_opt(c, FP_OPT_KPACK, 1) != 0;
 }
 
 int fp_pipe_soa_take(fp_ctx *c, size_t SC, fp_pipe_soa *soa) {
@@ -1438,8 +1456,8 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     uint8_t *rsn_s = (uint8_t *)fp_ws_take(c, SC);
     if (!ctl || !part || (nlinks && !gdata) || !asg_s || !rsn_s) return FP_ENOMEM;
     FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * LCTL * 4, st));
-    // buckets ride in s_idx when positions fit 21 bits (FLEETPLACE_NO_KPACK=1: search per stage)
-    const uint32_t kpack = fp_pipe_kpack(C);
+    // buckets ride in s_idx when positions fit 21 bits (FP_OPT_KPACK = 0: search per stage)
+    const uint32_t kpack = fp_pipe_kpack(c, C);
     GatherThr gth;
     memcpy(gth.t, tc, sizeof(uint32_t) * K);
     memcpy(gth.t + K, tm, sizeof(uint32_t) * K);
@@ -1473,15 +1491,14 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     // idle flushes: LDS rings always (producer and consumer share the workgroup); global links
     // only when bounded -- their consumer runs beside the producer and back-pressure bounds
     // the extra partial slots (an unbounded link is sized for full slots only).
-    // FLEETPLACE_PIPE_FLUSH = mask of the two (0 disables).
-    a.flush = geo.bounded ? 3u : 1u;
-    if (getenv("FLEETPLACE_PIPE_FLUSH")) a.flush &= (uint32_t)atoi(getenv("FLEETPLACE_PIPE_FLUSH"));
+    // FP_OPT_PIPE_FLUSH = mask of the two (0 disables).
+    a.flush = (geo.bounded ? 3u : 1u) & (uint32_t)fp_opt(c, FP_OPT_PIPE_FLUSH, 3);
     a.part = part;
     a.s_cpu = s_cpu; a.s_mem = s_mem; a.s_req = s_req; a.s_conf = s_conf; a.s_idx = s_idx;
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
     a.assign = asg_s; a.reason = rsn_s; a.cost = b->cost; a.err = c->d_err;
-    a.spin_ticks = SPIN_TICKS;
-    if (getenv("FLEETPLACE_SPIN_TICKS")) a.spin_ticks = strtoull(getenv("FLEETPLACE_SPIN_TICKS"), nullptr, 10);
+    a.spin_ticks = (uint64_t)fp_opt(c, FP_OPT_SPIN_TICKS, (int64_t)SPIN_TICKS);
+    a.sys = geo.sys;
     // bucket thresholds (fp_place.hip chooses them; any ascending choice with T0 = 0 is
     // exact -- it only decides how tight the candidate masks are)
     memcpy(a.tc, tc, sizeof(a.tc));
@@ -1514,6 +1531,15 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     return FP_OK;
 }
 
+// The pipeline fp_dev_place_batch runs for S x C x N on this ctx (fleetplace.h FP_GEOM_*).
+int fp_place_geometry_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t *out) {
+    PipeGeom g;
+    if (!pipe_geom(c, S, C, N, &g)) return FP_EOVERFLOW;
+    const uint32_t v[FP_GEOM_COUNT] = {g.G, g.W, g.B, g.R, g.lag, g.slots, g.bounded, g.resident, g.sys};
+    memcpy(out, v, sizeof(v));
+    return FP_OK;
+}
+
 #ifdef FP_PIPE_STATS
 extern "C" int fp_debug_pipe_timeline(unsigned long long *out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_tl), sizeof(unsigned long long) * 16 * TL_B * 8) != hipSuccess)
@@ -1542,20 +1568,6 @@ extern "C" int fp_debug_clock_ghz(fp_ctx *c, double *ghz) {
     (void)hipFree(d);
     if (!ok || !h[1]) return FP_EDEVICE;
     *ghz = (double)h[0] / (double)h[1] * 0.1;
-    return FP_OK;
-}
-// launch geometry fp_dev_place_batch picks for S x C x N: [0] G [1] W [2] B [3] R [4] lag
-// [5] link slots [6] bounded [7] resident segment slots on the device (occupancy x CUs)
-extern "C" int fp_debug_pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t *out) {
-    PipeGeom g;
-    if (!pipe_geom(c, S, C, N, &g)) return FP_EOVERFLOW;
-    int dev_cu = 0, occ = 0;
-    (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
-    const bool wide = wide_g(g.W, g.G);
-    const void *fn = wide ? kKernelWide[g.G / 4] : kKernel[g.G];
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(g.W * 64), g.lds);
-    const uint32_t v[8] = {g.G, g.W, g.B, g.R, g.lag, g.slots, g.bounded, (uint32_t)(occ * dev_cu)};
-    memcpy(out, v, sizeof(v));
     return FP_OK;
 }
 extern "C" int fp_debug_pipe_stats(unsigned long long *out, int reset) {

@@ -1,0 +1,251 @@
+// Systolic exact first fit of one 64-node group (k_ffd_pipe's group loop for long queues).
+//
+// The serial loop (fpp_group_x, fp_pipe_asm.h) checks one queued container per iteration
+// against all 64 nodes: ~172 cycles of a VALU -> SALU -> EXEC -> VALU dependency chain per
+// container, so a group that fills with ~480 containers keeps its stage busy for ~35 us and
+// the config-3 front advances one group at a time.
+//
+// Here the NODES travel instead: the group's live nodes (those that can take the batch's
+// smallest demands) are compacted into positions 0..L-1 and rotated one lane per step
+// (DPP wave_ror:1), while the queued containers sit still, compacted into lanes 0..Q-1 in
+// FFD order.  At step tau lane t holds position tau - t, so
+//   * container t tests positions 0, 1, 2, ... at steps t, t+1, t+2, ... (first fit order);
+//   * position p meets containers 0, 1, 2, ... at steps p, p+1, ... (FFD order),
+// and every (container, node) test sees exactly the placements of the earlier containers
+// on that node: the sequential first fit, bit for bit.  A step is ~20 wave instructions for
+// up to 64 tests, so a queue of Q containers that mostly fits costs ~Q + (first-fit
+// position) steps instead of Q serial checks.
+//
+// Containers still pending after `max_steps` finish in the serial loop with the node state
+// of that moment.  That is exact too: a pending container t has failed positions <= tau - t,
+// which stay infeasible (capacity only shrinks, SPEC.md 2.3), and every earlier pending
+// container is checked before it.
+#pragma once
+#include <stdint.h>
+
+#include "fp_pipe_asm.h"
+
+namespace fpp {
+
+// DPP wave_ror:1 -- lane i receives lane i-1, lane 0 receives lane 63
+__device__ __forceinline__ uint32_t sys_ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x13C, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t sys_push(uint32_t dst_lane, uint32_t v) {  // ds_permute_b32
+    return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst_lane << 2), (int)v);
+}
+__device__ __forceinline__ uint32_t sys_pull(uint32_t src_lane, uint32_t v) {  // ds_bpermute_b32
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+// OR over the wave of a 32-bit value (DPP row shifts + row broadcasts, then lane 63)
+__device__ __forceinline__ uint32_t sys_wave_or(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// One group's queue q (lanes = containers in FFD order; cpu/mem/req/conf per lane) against
+// the group's records (lane = node: rcf, rmf, rcu, rlab = ~labels).  qc/qm: the batch's
+// smallest cpu / mem demands (a superset bound: nodes below them are never live).
+// Returns in asg the node (gbg | l) of every placed queued lane and FP_NONE for the others
+// of q (left for the caller: misses, or `left` = still pending for the serial finish);
+// touched |= the nodes placed on.
+// The step loop (exact semantics of the FP_SYS_CXX loop above it in fpp_sys_group).
+// Phase A (tau < L): the window of started containers grows by one lane per step,
+// win = lanes 0..tau.  Phase B (tau >= L): it slides, win = lanes tau-L+1..tau, and
+// container tau - L, which has tested every live position, leaves `pend` (a miss).
+// Per step: exec = win & pend, three v_cmpx narrow it to the containers that fit the
+// position in their lane (EXEC = EXEC & test on gfx950), the placement is three VALU
+// ops under that exec, then the node records rotate one lane (DPP wave_ror:1).
+// The loop ends when pend is empty, or (phase B) after max_steps steps; on exit
+// tau = the rotations applied.  Wait states: a VALU write of a rotated register, and
+// v_cmpx's EXEC write, are >= 5 instructions ahead of the DPP reading it.
+// Assumes every lane of the wave is active (k_ffd_pipe's group loop).
+__device__ __forceinline__ void fpp_sys_steps(uint32_t &xc, uint32_t &xm, uint32_t &xu, uint32_t &xl, uint32_t kc,
+                                              uint32_t km, uint32_t kr, uint32_t kx, uint32_t &apos, uint64_t &pend,
+                                              uint32_t &tau, uint32_t L, uint32_t max_steps) {
+    uint64_t win = 0, esv;
+    uint32_t u = 0, t0;
+    asm volatile(
+        "s_mov_b64 %[esv], exec\n"
+        ".LsysA%=:\n\t"
+        "s_lshl_b64 %[win], %[win], 1\n\t"
+        "s_bitset1_b64 %[win], 0\n\t"
+        "s_and_b64 exec, %[win], %[pend]\n\t"
+        "v_cmpx_ge_u32_e32 vcc, %[xc], %[kc]\n\t"
+        "v_cmpx_ge_u32_e32 vcc, %[xm], %[km]\n\t"
+        "v_and_b32_e32 %[t0], %[xl], %[kr]\n\t"
+        "v_and_or_b32 %[t0], %[xu], %[kx], %[t0]\n\t"
+        "v_cmpx_eq_u32_e32 vcc, 0, %[t0]\n\t"
+        "v_sub_u32_e32 %[xc], %[xc], %[kc]\n\t"
+        "v_sub_u32_e32 %[xm], %[xm], %[km]\n\t"
+        "v_or_b32_e32 %[xu], %[xu], %[kx]\n\t"
+        "v_mov_b32_e32 %[apos], %[tau]\n\t"
+        "s_andn2_b64 %[pend], %[pend], exec\n\t"
+        "s_cbranch_scc0 .LsysEnd%=\n\t"
+        "s_mov_b64 exec, %[esv]\n\t"
+        "s_add_u32 %[tau], %[tau], 1\n\t"
+        "v_mov_b32_dpp %[xl], %[xl] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %[xc], %[xc] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %[xm], %[xm] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %[xu], %[xu] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_cmp_lt_u32 %[tau], %[L]\n\t"
+        "s_cbranch_scc1 .LsysA%=\n"
+        ".LsysB%=:\n\t"
+        "s_cmp_ge_u32 %[tau], %[cap]\n\t"
+        "s_cbranch_scc1 .LsysEnd%=\n\t"
+        "s_lshl_b64 %[win], %[win], 1\n\t"
+        "s_bitset0_b64 %[pend], %[u]\n\t"
+        "s_add_u32 %[u], %[u], 1\n\t"
+        "s_and_b64 exec, %[win], %[pend]\n\t"
+        "v_cmpx_ge_u32_e32 vcc, %[xc], %[kc]\n\t"
+        "v_cmpx_ge_u32_e32 vcc, %[xm], %[km]\n\t"
+        "v_and_b32_e32 %[t0], %[xl], %[kr]\n\t"
+        "v_and_or_b32 %[t0], %[xu], %[kx], %[t0]\n\t"
+        "v_cmpx_eq_u32_e32 vcc, 0, %[t0]\n\t"
+        "v_sub_u32_e32 %[xc], %[xc], %[kc]\n\t"
+        "v_sub_u32_e32 %[xm], %[xm], %[km]\n\t"
+        "v_or_b32_e32 %[xu], %[xu], %[kx]\n\t"
+        "v_mov_b32_e32 %[apos], %[tau]\n\t"
+        "s_add_u32 %[tau], %[tau], 1\n\t"
+        "s_andn2_b64 %[pend], %[pend], exec\n\t"
+        "s_mov_b64 exec, %[esv]\n\t"
+        "v_mov_b32_dpp %[xl], %[xl] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %[xc], %[xc] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %[xm], %[xm] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %[xu], %[xu] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_cbranch_scc1 .LsysB%=\n"
+        ".LsysEnd%=:\n\t"
+        "s_mov_b64 exec, %[esv]"
+        : [xc] "+v"(xc), [xm] "+v"(xm), [xu] "+v"(xu), [xl] "+v"(xl), [apos] "+v"(apos), [pend] "+s"(pend),
+          [tau] "+s"(tau), [win] "+s"(win), [u] "+s"(u), [esv] "=&s"(esv), [t0] "=&v"(t0)
+        : [kc] "v"(kc), [km] "v"(km), [kr] "v"(kr), [kx] "v"(kx), [L] "s"(L), [cap] "s"(max_steps)
+        : "scc", "vcc", "memory");
+    pend = fpp_uniform64(pend);
+    tau = (uint32_t)__builtin_amdgcn_readfirstlane((int)tau);
+}
+
+struct SysOut {
+    uint64_t left;  // queued lanes not resolved within max_steps (serial finish)
+};
+
+__device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
+                                                uint32_t &rmf, uint32_t &rcu, uint32_t rlab, uint32_t cpu,
+                                                uint32_t mem, uint32_t req, uint32_t conf, uint32_t gbg, uint32_t qc,
+                                                uint32_t qm, uint32_t max_steps) {
+    const uint32_t lane = __lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    SysOut out{0};
+    // live nodes: the batch corner (a node outside it fits no container of the batch, now or
+    // later) -> positions 0..L-1, in node order
+    const uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
+    const uint32_t L = (uint32_t)__builtin_popcountll(lm);
+    const bool inq = (q >> lane) & 1ull;
+    if (L == 0) {  // nothing can fit: every queued container misses the group
+        if (inq) asg = 0xFFFFFFFFu;
+        return out;
+    }
+    const uint32_t Q = (uint32_t)__builtin_popcountll(q);
+    // containers -> lanes 0..Q-1 (rank among the queued), the others after them
+    const uint32_t rq = inq ? (uint32_t)__builtin_popcountll(q & below) : Q + (uint32_t)__builtin_popcountll(~q & below);
+    const uint32_t kc = sys_push(rq, cpu), km = sys_push(rq, mem), kr = sys_push(rq, req), kx = sys_push(rq, conf);
+    const bool live = (lm >> lane) & 1ull;
+    const uint32_t pos = live ? (uint32_t)__builtin_popcountll(lm & below) : L + (uint32_t)__builtin_popcountll(~lm & below);
+    // position p starts at lane (64 - p) & 63: after tau rotations lane t holds position tau - t
+    const uint32_t at0 = (64u - pos) & 63u;
+    uint32_t xc = sys_push(at0, rcf), xm = sys_push(at0, rmf), xu = sys_push(at0, rcu), xl = sys_push(at0, rlab);
+    const uint32_t pmap = sys_push(pos, lane);  // lane p: the node lane of position p
+    if (((64u - lane) & 63u) >= L) {             // filler positions fit nothing
+        xc = 0u; xm = 0u; xu = 0xFFFFFFFFu; xl = 0xFFFFFFFFu;
+    }
+    uint64_t pend = Q >= 64 ? ~0ull : ((1ull << Q) - 1ull);  // compacted containers still open
+    uint32_t tau = 0;                                         // steps taken = rotations applied
+    uint32_t apos = 0xFFFFFFFFu;                              // step of the placement (compacted lane)
+#ifdef FP_SYS_CXX
+    uint64_t started = 0;
+    while (true) {
+        if (tau < 64) started |= 1ull << tau;
+        if (tau >= L && tau - L < 64) pend &= ~(1ull << (tau - L));  // tested every position: a miss
+        if (!pend || tau >= max_steps) break;
+        const uint64_t act = pend & started;
+        const uint64_t f1 = __builtin_amdgcn_ballot_w64(xc >= kc);
+        const uint64_t f2 = __builtin_amdgcn_ballot_w64(xm >= km);
+        const uint64_t f3 = __builtin_amdgcn_ballot_w64(((xl & kr) | (xu & kx)) == 0u);
+        const uint64_t fit = act & f1 & f2 & f3;
+        if ((fit >> lane) & 1ull) {
+            xc -= kc;
+            xm -= km;
+            xu |= kx;
+            apos = tau;
+        }
+        pend &= ~fit;
+        ++tau;
+        xc = sys_ror1(xc);
+        xm = sys_ror1(xm);
+        xu = sys_ror1(xu);
+        xl = sys_ror1(xl);
+    }
+    if (tau >= L && tau - L < 64) pend &= ~(1ull << (tau - L));
+#else
+    fpp_sys_steps(xc, xm, xu, xl, kc, km, kr, kx, apos, pend, tau, L, max_steps);
+#endif
+    // records back to node lanes: after tau rotations position p is at lane (tau - p) & 63
+    const uint32_t src = (tau - pos) & 63u;
+    const uint32_t ncf = sys_pull(src, xc), nmf = sys_pull(src, xm), ncu = sys_pull(src, xu);
+    if (live) { rcf = ncf; rmf = nmf; rcu = ncu; }
+    // placements: position -> node lane, then back to the container's own lane
+    if (apos != 0xFFFFFFFFu) apos = (apos - lane) & 63u;  // step -> position tested at that step
+    const uint32_t nl = sys_pull(apos & 63u, pmap);
+    const uint32_t cnode = apos != 0xFFFFFFFFu ? gbg + nl : 0xFFFFFFFFu;
+    const uint32_t back = sys_pull(rq, cnode);
+    const uint64_t pend_here = (uint64_t)sys_pull(rq, (uint32_t)((pend >> lane) & 1ull));  // pend bit of my rank
+    if (inq) asg = back;
+    out.left = __builtin_amdgcn_ballot_w64(inq && pend_here != 0);
+    // nodes placed on: OR of the one-hot node bits of the placed containers
+    const uint32_t bl = apos != 0xFFFFFFFFu && nl < 32 ? 1u << nl : 0u;
+    const uint32_t bh = apos != 0xFFFFFFFFu && nl >= 32 ? 1u << (nl - 32) : 0u;
+    touched |= ((uint64_t)sys_wave_or(bh) << 32) | sys_wave_or(bl);
+    return out;
+}
+
+// Steps the systolic phase runs past the queue length before the serial loop takes the
+// containers still open (measured: tools/ubench/systolic.hip)
+#ifndef FP_SYS_EXTRA
+#define FP_SYS_EXTRA 16
+#endif
+
+// Drop-in for fpp_group_x (same arguments): the systolic loop, the serial finish of what it
+// left open, and the same per-group vector epilogue (placed bits of the hits, next candidate
+// group of the misses).
+template <uint32_t g, uint32_t G>
+__device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint64_t &touched, uint32_t &asg,
+                                              uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
+                                              uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
+                                              uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
+                                              uint32_t &nhit, uint32_t qc, uint32_t qm) {
+    const uint32_t gbg = gb64 + g * 64u;
+    const SysOut so = fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm,
+                                    (uint32_t)__builtin_popcountll(q) + FP_SYS_EXTRA);
+    uint64_t left = fpp_uniform64(so.left);
+    touched = fpp_uniform64(touched);
+    if (left) fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
+    const uint32_t lane = __lane_id();
+    const bool inq = (q >> lane) & 1ull;
+    const uint64_t hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);
+#ifdef FP_PIPE_STATS
+    nhit += (uint32_t)__builtin_popcountll(hit);
+#else
+    (void)nhit;
+#endif
+    placed |= hit;
+    if (inq && asg == 0xFFFFFFFFu) {
+        const uint64_t above = (((uint64_t)cand_hi << 32) | cand) & ~((2ull << g) - 1ull);
+        nxt = above ? (uint32_t)__builtin_ctzll(above) : G;
+    }
+}
+
+}  // namespace fpp

@@ -14,7 +14,7 @@
 //   3. rocprim radix sort (stable) => (cpu desc, mem desc, index asc) per scenario:
 //      segmented per scenario when there are several (no scenario bits in the key),
 //      device-wide otherwise (or with the scenario field above the key when
-//      FLEETPLACE_NO_SEGSORT is set).
+//      FP_OPT_SEGSORT is 0).
 //   4. k_ffd_pipe   : (fp_pipe.hip) per scenario, containers in key order stream
 //                     through a pipeline of node-group stages (LDS-resident node
 //                     tiles); lowest feasible node wins, capacity updated in place.
@@ -712,10 +712,10 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         mbits = fp_bitwidth(dm - 1);
     }
     // Per-scenario LDS sort: dense ranks with at most 256 values per dimension and a
-    // scenario that fits LDS (C <= 51k).  FLEETPLACE_NO_SCEN_SORT=1 keeps the radix path.
+    // scenario that fits LDS (C <= 51k).  FP_OPT_SCEN_SORT = 0 keeps the radix path.
     const bool scen_sort = ranks && dc >= 1 && dm >= 1 && dc <= SS_DIG && dm <= SS_DIG &&
                            ss_lds_bytes(C) <= SS_LDS_CAP &&
-                           !(getenv("FLEETPLACE_NO_SCEN_SORT") && atoi(getenv("FLEETPLACE_NO_SCEN_SORT")));
+                           fp_opt(c, FP_OPT_SCEN_SORT, 1) != 0;
     if (scen_sort) {
         uint32_t tc[FP_BUCKETS], tm[FP_BUCKETS];
         {
@@ -736,7 +736,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
             FP_HIP(hipGetLastError());
         }
         ScenSortArgs sa;
-        sa.C = C; sa.dc = dc; sa.dm = dm; sa.kpack = fp_pipe_kpack(C);
+        sa.C = C; sa.dc = dc; sa.dm = dm; sa.kpack = fp_pipe_kpack(c, C);
         sa.dig = dig;
         sa.cval = rval; sa.mval = rval + RANK_MAX_VALUE;
         fp_pipe_soa soa;
@@ -763,7 +763,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         k_iota_vals<<<grid_for(SC, 256), 256, 0, st>>>(SC, C, vals_out);
         FP_HIP(hipGetLastError());
         order = vals_out;
-    } else if (kbits <= 32 && S > 1 && !getenv("FLEETPLACE_NO_SEGSORT")) {
+    } else if (kbits <= 32 && S > 1 && fp_opt(c, FP_OPT_SEGSORT, 1) != 0) {
         // many scenarios: per-scenario segments, so the key holds no scenario field (config 4:
         // 15 bits of radix instead of 27; sort 7.3 -> 5.4 ms for 4096 x 50k)
         uint32_t *k_in = (uint32_t *)keys_in, *k_out = (uint32_t *)keys_out;

@@ -69,6 +69,25 @@ class Planner:
     def profile(self, enable=True):
         check(self._L.fp_ctx_profile(self._ctx, int(enable)), "fp_ctx_profile")
 
+    def set_option(self, name: str, value: int = _lib.FP_OPT_AUTO):
+        """fp_ctx_set_option by name (_lib.OPTIONS); FP_OPT_AUTO (-1) restores the default."""
+        check(self._L.fp_ctx_set_option(self._ctx, _lib.OPTIONS[name], int(value)), f"fp_ctx_set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = ct.c_int64()
+        check(self._L.fp_ctx_get_option(self._ctx, _lib.OPTIONS[name], ct.byref(v)), f"fp_ctx_get_option({name})")
+        return int(v.value)
+
+    def reset_options(self):
+        for name in _lib.OPTIONS:
+            self.set_option(name, _lib.FP_OPT_AUTO)
+
+    def geometry(self, S: int, C: int, N: int) -> dict:
+        """The placement pipeline a batch of S x C x N runs on this context (fp_place_geometry)."""
+        out = (ct.c_uint32 * len(_lib.GEOM_FIELDS))()
+        check(self._L.fp_place_geometry(self._ctx, S, C, N, out), "fp_place_geometry")
+        return dict(zip(_lib.GEOM_FIELDS, (int(x) for x in out)))
+
     def kernel_stats(self, kernel_id: int):
         ms = ct.c_double()
         n = ct.c_uint64()

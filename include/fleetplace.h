@@ -123,6 +123,33 @@ enum { FP_K_PLACE = 0, FP_K_SORT = 1, FP_K_FEAS = 2, FP_K_LEVEL = 3, FP_K_GEN = 
 int fp_ctx_profile(fp_ctx *ctx, int enable);
 int fp_ctx_kernel_stats(fp_ctx *ctx, int kernel_id, double *total_ms, uint64_t *launches);
 
+/* Per-context tuning / test options.  FP_OPT_AUTO (-1) = the production choice (the
+ * default of every option).  Nothing is read from the environment: an option changes
+ * only the context it is set on.  The pipeline geometry options are hints a shape may
+ * not be able to serve (the planner then falls back to the nearest valid geometry);
+ * fp_place_geometry reports what a call will run.  Results are bit-exact whatever the
+ * options (only the work schedule changes), except FP_OPT_SPIN_TICKS, which can make a
+ * call fail with FP_EDEVICE. */
+#define FP_OPT_AUTO (-1)
+enum fp_option {
+    FP_OPT_PIPE_W = 0,        /* stages (waves) per segment, >= 1                         */
+    FP_OPT_PIPE_SEG = 1,      /* 64-node groups per segment, 1..40                         */
+    FP_OPT_PIPE_R = 2,        /* LDS ring depth between stages, 2..6                        */
+    FP_OPT_PIPE_LAG = 3,      /* segment ticket lag (0 = segments side by side)            */
+    FP_OPT_LINK_SLOTS = 4,    /* bounded global link ring slots, >= 8                       */
+    FP_OPT_LINK_BOUNDED = 5,  /* 0 = links hold every container, 1 = bounded rings          */
+    FP_OPT_PIPE_FLUSH = 6,    /* idle-flush mask: bit 0 LDS rings, bit 1 global links      */
+    FP_OPT_SPIN_TICKS = 7,    /* deadlock guard in 100 MHz ticks (auto: 60 s)               */
+    FP_OPT_KPACK = 8,         /* 0 = bucket search per stage instead of packed buckets      */
+    FP_OPT_SCEN_SORT = 9,     /* 0 = radix-key FFD order instead of the per-scenario LDS sort */
+    FP_OPT_SEGSORT = 10,      /* 0 = device-wide radix sort instead of segmented            */
+    FP_OPT_SYSTOLIC = 11,     /* systolic group fill for queues of >= value containers (0 = off) */
+    FP_OPT_LEVELIZE_SYNC = 12,/* 1 = level-synchronous Kahn instead of the async levelizer */
+    FP_OPT_COUNT = 13
+};
+int fp_ctx_set_option(fp_ctx *ctx, int option, int64_t value);
+int fp_ctx_get_option(fp_ctx *ctx, int option, int64_t *value);
+
 /* ---- host-pointer API (drop-in, synchronous) ---------------------------- */
 /* A1 engine.rs:67-85: perm_out = stable partition (has_deps == 0 first). */
 int fp_legacy_order(fp_ctx *ctx, const fp_graph *g, uint32_t *perm_out);
@@ -151,6 +178,12 @@ int fp_dev_place_batch(fp_ctx *ctx, const fp_batch *b);
  * (the pipeline's link sizing follows its occupancy). */
 int fp_place_ws_bytes(fp_ctx *ctx, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes,
                       uint64_t *bytes_out);
+/* The placement pipeline a batch of n_scen x n_containers x n_nodes runs on this ctx and
+ * device (options included): out[FP_GEOM_*]. */
+enum { FP_GEOM_GROUPS = 0, FP_GEOM_STAGES = 1, FP_GEOM_SEGMENTS = 2, FP_GEOM_RING = 3, FP_GEOM_LAG = 4,
+       FP_GEOM_LINK_SLOTS = 5, FP_GEOM_BOUNDED = 6, FP_GEOM_RESIDENT = 7, FP_GEOM_SYSTOLIC = 8,
+       FP_GEOM_COUNT = 9 };
+int fp_place_geometry(fp_ctx *ctx, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes, uint32_t *out);
 int fp_dev_feasibility(fp_ctx *ctx, const fp_containers *c, const fp_nodes *nodes,
                        uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out);
 /* Stage 2 batched over what-if scenarios: for each scenario s and container c of b

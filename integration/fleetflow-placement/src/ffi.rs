@@ -20,6 +20,30 @@ pub const FP_K_SORT: c_int = 1;
 pub const FP_K_FEAS: c_int = 2;
 pub const FP_K_LEVEL: c_int = 3;
 pub const FP_K_GEN: c_int = 4;
+pub const FP_OPT_AUTO: i64 = -1;
+pub const FP_OPT_PIPE_W: c_int = 0;
+pub const FP_OPT_PIPE_SEG: c_int = 1;
+pub const FP_OPT_PIPE_R: c_int = 2;
+pub const FP_OPT_PIPE_LAG: c_int = 3;
+pub const FP_OPT_LINK_SLOTS: c_int = 4;
+pub const FP_OPT_LINK_BOUNDED: c_int = 5;
+pub const FP_OPT_PIPE_FLUSH: c_int = 6;
+pub const FP_OPT_SPIN_TICKS: c_int = 7;
+pub const FP_OPT_KPACK: c_int = 8;
+pub const FP_OPT_SCEN_SORT: c_int = 9;
+pub const FP_OPT_SEGSORT: c_int = 10;
+pub const FP_OPT_SYSTOLIC: c_int = 11;
+pub const FP_OPT_LEVELIZE_SYNC: c_int = 12;
+pub const FP_GEOM_GROUPS: usize = 0;
+pub const FP_GEOM_STAGES: usize = 1;
+pub const FP_GEOM_SEGMENTS: usize = 2;
+pub const FP_GEOM_RING: usize = 3;
+pub const FP_GEOM_LAG: usize = 4;
+pub const FP_GEOM_LINK_SLOTS: usize = 5;
+pub const FP_GEOM_BOUNDED: usize = 6;
+pub const FP_GEOM_RESIDENT: usize = 7;
+pub const FP_GEOM_SYSTOLIC: usize = 8;
+pub const FP_GEOM_COUNT: usize = 9;
 
 /// Opaque `fp_ctx` (one per host thread; owns a HIP stream on one MI355X).
 #[repr(C)]
@@ -91,6 +115,8 @@ unsafe extern "C" {
     pub fn fp_abi_version() -> c_int;
     pub fn fp_ctx_profile(ctx: *mut fp_ctx, enable: c_int) -> c_int;
     pub fn fp_ctx_kernel_stats(ctx: *mut fp_ctx, kernel_id: c_int, total_ms: *mut f64, launches: *mut u64) -> c_int;
+    pub fn fp_ctx_set_option(ctx: *mut fp_ctx, option: c_int, value: i64) -> c_int;
+    pub fn fp_ctx_get_option(ctx: *mut fp_ctx, option: c_int, value: *mut i64) -> c_int;
 
     pub fn fp_legacy_order(ctx: *mut fp_ctx, g: *const fp_graph, perm_out: *mut u32) -> c_int;
     pub fn fp_levelize(ctx: *mut fp_ctx, g: *const fp_graph, level_out: *mut u32, order_out: *mut u32,
@@ -107,6 +133,8 @@ unsafe extern "C" {
     pub fn fp_dev_place_batch(ctx: *mut fp_ctx, b: *const fp_batch) -> c_int;
     pub fn fp_place_ws_bytes(ctx: *mut fp_ctx, n_scen: u32, n_containers: u32, n_nodes: u32,
                              bytes_out: *mut u64) -> c_int;
+    pub fn fp_place_geometry(ctx: *mut fp_ctx, n_scen: u32, n_containers: u32, n_nodes: u32,
+                             out: *mut u32) -> c_int;
     pub fn fp_dev_feasibility(ctx: *mut fp_ctx, c: *const fp_containers, nodes: *const fp_nodes,
                               first_out: *mut u32, count_out: *mut u32, bitmap_out: *mut u64) -> c_int;
     pub fn fp_dev_feasibility_batch(ctx: *mut fp_ctx, b: *const fp_batch, first_out: *mut u32,

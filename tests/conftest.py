@@ -49,3 +49,14 @@ def planner():
     p = Planner(0)
     yield p
     p.close()
+
+
+@pytest.fixture
+def opts(planner):
+    """Set context options for one test (fp_ctx_set_option, fleetplace.h enum fp_option):
+    ``opts(pipe_w=4, pipe_seg=4)``.  Every option goes back to FP_OPT_AUTO afterwards."""
+    def set_(**kw):
+        for k, v in kw.items():
+            planner.set_option(k, v)
+    yield set_
+    planner.reset_options()

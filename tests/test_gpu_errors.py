@@ -8,8 +8,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_pipeline_deadlock_guard_is_reported_by_sync(planner, monkeypatch):
-    """Force the placement pipeline's wall-clock guard (FLEETPLACE_SPIN_TICKS=1: any
+def test_pipeline_deadlock_guard_is_reported_by_sync(planner, opts):
+    """Force the placement pipeline's wall-clock guard (FP_OPT_SPIN_TICKS = 1: any
     wait longer than ~2k spin iterations aborts): the launch drains, fp_dev_place_batch
     itself returns OK (asynchronous), fp_ctx_sync reports FP_EDEVICE exactly once, and a
     normal run afterwards is clean."""
@@ -19,13 +19,13 @@ def test_pipeline_deadlock_guard_is_reported_by_sync(planner, monkeypatch):
     db = DevBatch.allocate(4, 50_000, 5_000, "cuda:0")
     planner.dev_gen_batch(0x5EED0004, db, 7)
     snap = db.node_snapshot()
-    monkeypatch.setenv("FLEETPLACE_SPIN_TICKS", "1")
+    opts(spin_ticks=1)
     planner.dev_place_batch(db)
     with pytest.raises(FleetplaceError) as e:
         planner.sync()
     assert e.value.code == FP_EDEVICE
     planner.sync()  # reported once, then cleared
-    monkeypatch.delenv("FLEETPLACE_SPIN_TICKS")
+    planner.set_option("spin_ticks")
     db.restore_nodes(snap)
     planner.dev_place_batch(db)
     planner.sync()

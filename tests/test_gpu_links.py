@@ -31,22 +31,22 @@ def _check(planner, O, cont, nodes):
 
 @pytest.mark.parametrize("slots", ["8", "9", "64"])
 @pytest.mark.parametrize("C,N", [(60_000, 12_000), (20_000, 30_000)])
-def test_small_ring_single_scenario(C, N, slots, planner, O, monkeypatch):
+def test_small_ring_single_scenario(C, N, slots, planner, O, opts):
     """One scenario, narrow geometry (segments of four one-group stages: 47-118
     segments), links of 8/9/64 slots of 64 containers."""
-    monkeypatch.setenv("FLEETPLACE_LINK_SLOTS", slots)
+    opts(link_slots=int(slots))
+    assert planner.geometry(1, C, N)["bounded"] == 1
     cont, nodes = O.gen_scenario(SEED + C + N, 0, C, N, 7)
     _check(planner, O, cont, nodes)
 
 
 @pytest.mark.parametrize("w,seg", [("4", "4"), ("1", "12"), ("1", "32")])
-def test_small_ring_batch(w, seg, planner, O, monkeypatch):
+def test_small_ring_batch(w, seg, planner, O, opts):
     """A few scenarios (all segments resident: lag 0, bounded links) in the narrow and
     one-wave geometries, 8-slot rings."""
-    monkeypatch.setenv("FLEETPLACE_LINK_SLOTS", "8")
-    monkeypatch.setenv("FLEETPLACE_PIPE_W", w)
-    monkeypatch.setenv("FLEETPLACE_PIPE_SEG", seg)
+    opts(link_slots=8, pipe_w=int(w), pipe_seg=int(seg))
     S, C, N, base = 4, 12_000, 6_000, 3
+    assert planner.geometry(S, C, N)["bounded"] == 1
     conts, nodes = [], []
     for s in range(S):
         c, n = O.gen_scenario(SEED + 5, base + s, C, N, 7)

@@ -495,10 +495,9 @@ GEOMETRIES = {"wide": ("4", "40"), "narrow": ("4", "4"), "one-stage": ("1", "16"
 
 
 @pytest.fixture(params=sorted(GEOMETRIES))
-def geometry(request, monkeypatch):
+def geometry(request, opts):
     w, seg = GEOMETRIES[request.param]
-    monkeypatch.setenv("FLEETPLACE_PIPE_W", w)
-    monkeypatch.setenv("FLEETPLACE_PIPE_SEG", seg)
+    opts(pipe_w=int(w), pipe_seg=int(seg))
     return request.param
 
 

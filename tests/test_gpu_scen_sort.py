@@ -18,8 +18,8 @@ SS_MAX_C = 50_680
 
 
 @pytest.fixture(params=["scen_sort", "radix"])
-def sort_path(request, monkeypatch):
-    monkeypatch.setenv("FLEETPLACE_NO_SCEN_SORT", "1" if request.param == "radix" else "0")
+def sort_path(request, opts):
+    opts(scen_sort=0 if request.param == "radix" else -1)
     return request.param
 
 

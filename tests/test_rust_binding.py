@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "include", "fleetplace.h")
 FFI = os.path.join(ROOT, "integration", "fleetflow-placement", "src", "ffi.rs")
 
-C2R = {"uint32_t": "u32", "uint8_t": "u8", "uint64_t": "u64", "int": "c_int", "double": "f64", "void": "c_void",
+C2R = {"uint32_t": "u32", "uint8_t": "u8", "uint64_t": "u64", "int64_t": "i64", "int": "c_int", "double": "f64", "void": "c_void",
        "char": "c_char", "fp_ctx": "fp_ctx", "fp_graph": "fp_graph", "fp_containers": "fp_containers",
        "fp_nodes": "fp_nodes", "fp_batch": "fp_batch"}
 
@@ -104,6 +104,11 @@ def test_constants_match():
         assert re.search(rf"pub const {name}: u8 = {val};", rs), name
     for name, val in re.findall(r"(FP_K_(?!COUNT)\w+) = (\d+)", src):
         assert re.search(rf"pub const {name}: c_int = {val};", rs), name
+    for name, val in re.findall(r"(FP_OPT_(?!COUNT)\w+) = (\d+)", src):
+        assert re.search(rf"pub const {name}: c_int = {val};", rs), name
+    for name, val in re.findall(r"(FP_GEOM_\w+) = (\d+)", src):
+        assert re.search(rf"pub const {name}: usize = {val};", rs), name
+    assert "pub const FP_OPT_AUTO: i64 = -1;" in rs
 
 
 def test_build_script_compiles_every_library_source():

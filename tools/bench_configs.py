@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import DevBatch, Planner  # noqa: E402
 from fleetflow_amd._lib import FP_K_FEAS, FP_K_LEVEL, FP_K_PLACE, FP_K_SORT  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (checker / CPU baseline only)
@@ -168,6 +169,7 @@ def main():
     cpu = not args.no_cpu
     only = set(args.only.split(","))
     with Planner(0) as p:
+        _opts.apply_env(p)
         if "2" in only:
             print(json.dumps(ffd_config(p, dev, "2: 10k services x 1k servers, cpu/mem/ports", SEED + 2,
                                         10_000, 1_000, 1, args.reps, cpu)), flush=True)

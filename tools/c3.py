@@ -15,10 +15,12 @@ CHILD = r"""
 import sys, hashlib
 sys.path.insert(0, %r)
 import torch
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import DevBatch, Planner
 from fleetflow_amd._lib import FP_K_PLACE
 C, N = int(%r), int(%r)
 p = Planner(0)
+_opts.apply_env(p)
 db = DevBatch.allocate(1, C, N, "cuda:0")
 p.dev_gen_batch(0x5EED0003, db, 7)
 p.sync()

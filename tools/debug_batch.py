@@ -12,6 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import DevBatch, Planner  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
@@ -54,6 +55,7 @@ def run(p, S, C, N, base=1024):
 def main():
     a = [int(x) for x in sys.argv[1:]]
     p = Planner(0)
+    _opts.apply_env(p)
     print("lib", os.environ.get("FLEETPLACE_LIB", "default"), "W", os.environ.get("FLEETPLACE_PIPE_W"),
           "SEG", os.environ.get("FLEETPLACE_PIPE_SEG"), flush=True)
     for i in range(0, len(a), 3):

@@ -2,10 +2,12 @@
 import os, sys, time, json
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 import torch
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import DevBatch, Planner, _lib
 for N in (3000, 1500):
     S, C = 512, 50000
     p = Planner(0)
+    _opts.apply_env(p)
     db = DevBatch.allocate(S, C, N, "cuda:0")
     p.dev_gen_batch(0x5EED0004, db, 7)
     snap = db.node_snapshot()

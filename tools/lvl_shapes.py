@@ -10,6 +10,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import Planner  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (input generator only)
 
@@ -37,6 +38,7 @@ def run(p, dev, shape):
 def main():
     dev = torch.device("cuda", 0)
     with Planner(0) as p:
+        _opts.apply_env(p)
         for shape in [(1000, 500, 0, 0, 0), (1, 500, 0, 0, 0), (1000, 100, 0, 0, 0), (100, 1, 50, 10_000, 0),
                       (1000, 500, 50, 10_000, 333)]:
             print(json.dumps(run(p, dev, shape)), flush=True)

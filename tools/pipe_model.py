@@ -29,6 +29,7 @@ os.environ.setdefault("FLEETPLACE_LIB", os.path.join(ROOT, "fleetflow_amd", "lib
 
 import torch  # noqa: E402
 
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import DevBatch, Planner, _lib  # noqa: E402
 
 # (leg, scenarios in the diagnostics run, C, N, seed)
@@ -111,6 +112,7 @@ def front_model(p, kms):
 def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pipe_model.json")
     p = Planner(0)
+    _opts.apply_env(p)
     clk = clock_ghz(p)
     latest, raw = {}, {"clock_ghz": clk}
     for leg, S, C, N, seed in LEGS:

@@ -13,6 +13,7 @@ os.environ.setdefault("FLEETPLACE_LIB", os.path.join(ROOT, "fleetflow_amd", "lib
 
 import torch  # noqa: E402
 
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import DevBatch, Planner, _lib  # noqa: E402
 
 
@@ -20,6 +21,7 @@ def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     C, N = int(os.environ.get("C", 50000)), int(os.environ.get("N", 5000))
     p = Planner(0)
+    _opts.apply_env(p)
     db = DevBatch.allocate(S, C, N, "cuda:0")
     p.dev_gen_batch(0x5EED0004, db, 7)
     p.sync()  # the generator runs on the planner stream; torch copies on its own

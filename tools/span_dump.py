@@ -11,9 +11,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("FLEETPLACE_LIB", os.path.join(ROOT, "fleetflow_amd", "libfleetplace_stats.so"))
 import torch  # noqa: E402
+import _opts  # noqa: E402  (tools/_opts.py)
 from fleetflow_amd import DevBatch, Planner, _lib  # noqa: E402
 
 p = Planner(0)
+_opts.apply_env(p)
 C, N = 1_000_000, 100_000
 db = DevBatch.allocate(1, C, N, "cuda:0")
 p.dev_gen_batch(0x5EED0003, db, 7)
