@@ -23,10 +23,15 @@ the measured time with checks x cycles-per-check from the diagnostics build
 (profiles/pipe_model_latest.json).  The 16 B x S*C*N figure is reported under
 `work_equivalent`, labelled as what it is.
 
-A second leg, `config3`, times BASELINE configs[2] (1 scenario x 1M containers x
-100k nodes, the north-star sweep) on rank 0 at N = 1; a third, `stage2`, the
-scenario-batched feasibility/score sweep (fp_dev_feasibility_batch) against the
-VALU roofline.
+Legs in the same JSON line (rank 0 at N = 1; single scenarios are replicas, they do not shard):
+  config2   BASELINE configs[1]: 1 x 10k services x 1k servers (cpu/mem/ports)
+  config3   BASELINE configs[2]: 1 x 1M containers x 100k nodes, the north-star sweep
+  config5   BASELINE configs[4]: levelize the 1M-vertex depends_on DAG ((V+E)/s, roofline
+            on 16V + 12E + 4 bytes), then place its containers on 100k nodes with the levels
+  stage2    the scenario-batched feasibility/score sweep against the VALU roofline
+  cpu_baseline       the oracle FFD on config-4 scenarios on every usable host core
+  cpu_single_thread  the single-threaded C oracle on the same inputs as configs 2, 3 and 5
+                     (A1 legacy order, levels, FFD), each GPU result checked bit for bit
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -47,6 +52,9 @@ sys.path.insert(0, ROOT)
 
 C4, N4, S4, SEED4 = 50_000, 5_000, 4096, 0x5EED0004
 C3, N3, SEED3 = 1_000_000, 100_000, 0x5EED0003
+C2, N2, SEED2, FLAGS2 = 10_000, 1_000, 0x5EED0002, 1
+N5, SEED5 = 100_000, 0x5EED0005
+DAG5 = (1000, 500, 50, 10_000, 333)  # chains, chain length, fan-out layers, layer width, 3-cycles
 FLAGS = 7
 HBM_PEAK_GBPS = 8000.0
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -60,11 +68,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scenarios", type=int, default=S4, help="total what-if scenarios (config 4: 4096)")
     ap.add_argument("--config3-steps", type=int, default=3)
-    ap.add_argument("--no-config3", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="skip the config 2 / 3 / 5 legs")
     ap.add_argument("--no-stage2", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0, help="CPU baseline sample budget (wall s)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="host threads for the CPU baseline (default: min(16, usable cores); the GPU box grants 16/GPU)")
+                    help="host threads for the CPU baseline (default: every usable core, within the cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-launch", action="store_true",
                     help="test hook: each rank prints its rank/world env as JSON and exits (no GPU call)")
@@ -81,7 +89,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n):
+def launch_ranks(n, poll_s=0.2):
+    """Start n rank processes and wait for all of them.  If one exits non-zero (an OOM, an
+    FP_E* error, an assertion) the others would block in their next collective forever, so
+    they are terminated (then killed) and the launcher exits with the failing rank's code."""
     port = str(_free_port())
     procs = []
     for r in range(n):
@@ -89,9 +100,25 @@ def launch_ranks(n):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
-    for p in procs:
-        code = p.wait()
-        rc = rc or code
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code and not rc:
+                rc = code
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 10
+                for q in live:
+                    try:
+                        q.wait(max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+        if live:
+            time.sleep(poll_s)
     return rc
 
 
@@ -107,6 +134,23 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def _cpu_quota():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota if any."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return usable, quota, (min(usable, quota) if quota else usable)
 
 
 def cpu_baseline(budget_s, threads):
@@ -135,16 +179,72 @@ def cpu_baseline(budget_s, threads):
             if len(rates) >= 200:
                 break
         wall = time.perf_counter() - t_start
-    try:
-        usable = len(os.sched_getaffinity(0))
-    except AttributeError:
-        usable = os.cpu_count()
+    usable, quota, _ = _cpu_quota()
     return {"value": statistics.median(rates), "unit": "evals/s", "cores": threads, "kind": "port",
             "single_thread_value": statistics.median(singles),
-            "nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": _cpu_model(),
+            "nproc": os.cpu_count(), "usable_cpus": usable, "cgroup_cpu_quota": quota, "cpu_model": _cpu_model(),
             "sample": f"{len(rates)} waves of {threads} whole 50k x 5k config-4 scenarios on {threads} host "
                       f"threads (oracle/fp_oracle.c fpo_place: sort + first-fit scan), median wave rate, "
                       f"{wall:.1f} s timed after 1 warm-up wave; single-thread = median of 3 scenarios"}
+
+
+def _median_ms(fn, reps):
+    ts, out = [], None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return statistics.median(ts), out
+
+
+def cpu_single_thread_legs(gpu):
+    """the single-threaded C oracle on the same inputs as the GPU legs, timed on
+    this host (steady clock; median of 5 after a warm-up where a run is short, one run for the
+    ~35 s config-3 / config-5 FFD), and every GPU result checked against it bit for bit:
+      A1 legacy order (engine.rs:67-85) and Kahn levels on config 5's DAG, FFD of configs 2, 3
+      and 5b.  The two long FFD runs go on two host threads side by side (one core each)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    from oracle import oracle as O  # checker and CPU baseline only
+    O.lib()
+    out = {}
+    rp, col, hd = gpu["config5"]["graph"]
+    O.legacy_order(hd)
+    a1_ms, _ = _median_ms(lambda: O.legacy_order(hd), 5)
+    O.levelize(rp, col, hd)
+    lv_ms, (el, eo, en) = _median_ms(lambda: O.levelize(rp, col, hd), 5)
+    gl, go, gn = gpu["config5"]["levels"]
+    lv_ok = bool(np.array_equal(gl, el) and np.array_equal(go, eo) and gn == en)
+    V, E = hd.size, col.size
+    out["legacy_order_config5"] = {"ms": a1_ms, "unit_value": V / (a1_ms / 1e3), "unit": "vertices/s", "cores": 1}
+    out["levelize_config5"] = {"ms": lv_ms, "unit_value": (V + E) / (lv_ms / 1e3), "unit": "(V+E)/s", "cores": 1,
+                               "gpu_bit_exact": lv_ok}
+    cont2, nodes2 = O.gen_scenario(SEED2, 0, C2, N2, FLAGS2)
+    O.place(cont2, nodes2)
+    c2_ms, (ea, er, _, _) = _median_ms(lambda: O.place(cont2, nodes2), 5)
+    c2_ok = bool(np.array_equal(gpu["config2"]["plan"][0], ea) and np.array_equal(gpu["config2"]["plan"][1], er))
+    out["ffd_config2"] = {"ms": c2_ms, "unit_value": C2 * N2 / (c2_ms / 1e3), "unit": "evals/s", "cores": 1,
+                          "gpu_bit_exact": c2_ok}
+
+    def long_ffd(name, seed, C, N, level):
+        cont, nodes = O.gen_scenario(seed, 0, C, N, FLAGS)
+        ms, (ea, er, _, _) = _median_ms(lambda: O.place(cont, nodes, level=level), 1)
+        plan = gpu[name]["plan"]
+        return name, ms, C * N, bool(np.array_equal(plan[0], ea) and np.array_equal(plan[1], er))
+
+    with ThreadPoolExecutor(2) as ex:
+        jobs = [ex.submit(long_ffd, "config3", SEED3, C3, N3, None),
+                ex.submit(long_ffd, "config5", SEED5, V, N5, el)]
+        for j in jobs:
+            name, ms, evals, ok = j.result()
+            out[f"ffd_{name}"] = {"ms": ms, "unit_value": evals / (ms / 1e3), "unit": "evals/s", "cores": 1,
+                                  "gpu_bit_exact": ok}
+    bad = [k for k, v in out.items() if v.get("gpu_bit_exact") is False]
+    if bad:
+        raise RuntimeError(f"GPU results differ from the oracle: {bad}")
+    return out
 
 
 # ---------------------------------------------------------------------------------------------
@@ -214,14 +314,18 @@ def timed(steps, step, sync, barrier):
     return time.perf_counter() - t0
 
 
-def config3_leg(planner, dev, steps, warmup):
-    """BASELINE configs[2]: 1 x 1M containers x 100k nodes, flags 7 (a replica per GPU)."""
+def single_leg(planner, dev, leg, seed, C, N, flags, steps, warmup, level_t=None):
+    """One scenario (a replica per GPU; BASELINE configs 2, 3 and 5b): device-generated inputs
+    (SPEC.md 3, the generator of fp_dev_gen_batch), one step = restore the pristine node table +
+    dev_place_batch.  Returns the leg's record and its plan (host copies, for the oracle check)."""
     import torch
 
     from fleetflow_amd import DevBatch
     from fleetflow_amd._lib import FP_K_PLACE, FP_K_SORT
-    db = DevBatch.allocate(1, C3, N3, dev)
-    planner.dev_gen_batch(SEED3, db, FLAGS)
+    db = DevBatch.allocate(1, C, N, dev, with_level=level_t is not None)
+    planner.dev_gen_batch(seed, db, flags)
+    if level_t is not None:
+        db.level.copy_(level_t)
     pristine = db.node_snapshot()
 
     def step():
@@ -236,22 +340,66 @@ def config3_leg(planner, dev, steps, warmup):
     el = timed(steps, step, lambda: torch.cuda.synchronize(dev), lambda: None)
     planner.sync()
     if not torch.equal(db.assign, ref):
-        raise RuntimeError("config 3: timed steps did not reproduce the warmup plan")
+        raise RuntimeError(f"{leg}: timed steps did not reproduce the warmup plan")
     k_ms, k_n = planner.kernel_stats(FP_K_PLACE)
     s_ms, s_n = planner.kernel_stats(FP_K_SORT)
     planner.profile(False)
     step_s = el / steps
     kernel_s = k_ms / max(k_n, 1) / 1e3
-    placed = int((db.reason == 0).sum().item())
-    out = {"workload": "BASELINE config 3: 1 scenario x 1M containers x 100k nodes, ports+anti-affinity+labels",
-           "value": C3 * N3 / step_s, "unit": "evals/s (work-equivalent)", "ms_per_step": step_s * 1e3,
-           "steps": steps, "placed": placed, "nofit": C3 - placed,
+    reason = db.reason.cpu().numpy()
+    plan = (db.assign.cpu().numpy().view("uint32"), reason)
+    placed = int((reason == 0).sum())
+    out = {"value": C * N / step_s, "unit": "evals/s (work-equivalent)", "ms_per_step": step_s * 1e3,
+           "steps": steps, "placed": placed, "nofit": int((reason == 1).sum()), "cycle": int((reason == 2).sum()),
            "breakdown_ms": {"ffd_kernel": kernel_s * 1e3, "sort": s_ms / max(s_n, 1)},
-           "ns_per_container": step_s / C3 * 1e9,
-           "roofline": roofline("config3", 1, C3, N3, kernel_s, step_s)}
+           "ns_per_container": step_s / C * 1e9,
+           "geometry": planner.geometry(1, C, N),
+           "roofline": roofline(leg, 1, C, N, kernel_s, step_s)}
     del db, pristine
     torch.cuda.empty_cache()
-    return out
+    return out, plan
+
+
+def levelize_leg(planner, dev, steps):
+    """BASELINE config 5a: Kahn levels of the 1M-vertex depends_on DAG (SPEC.md 3.3: 1000 chains
+    x 500, 50 fan-out layers x 10k, 333 injected 3-cycles; host-generated by fleetflow_amd.synth,
+    CSR resident in HBM).  Roofline on SURVEY 8(d)'s 16V + 12E + 4 algorithmic bytes."""
+    import numpy as np
+    import torch
+
+    from fleetflow_amd import synth
+    from fleetflow_amd._lib import FP_K_LEVEL
+    rp, col, hd = synth.gen_dag(SEED5, *DAG5)
+    V, E = hd.size, col.size
+    to = lambda a: torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).to(dev)  # noqa: E731
+    rp_t, col_t, hd_t = to(rp), to(col), to(hd)
+    level_t = torch.empty(V, dtype=torch.int32, device=dev)
+    order_t = torch.empty(V, dtype=torch.int32, device=dev)
+    ncyc_t = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def step():
+        planner.dev_levelize(rp_t, col_t, hd_t, level_t, order_t, ncyc_t)
+
+    step()
+    planner.sync()
+    planner.profile(True)
+    el = timed(steps, step, lambda: torch.cuda.synchronize(dev), lambda: None)
+    planner.sync()
+    k_ms, k_n = planner.kernel_stats(FP_K_LEVEL)
+    planner.profile(False)
+    step_s, kernel_s = el / steps, k_ms / max(k_n, 1) / 1e3
+    nbytes = 16 * V + 12 * E + 4
+    levels = level_t.cpu().numpy().view(np.uint32)
+    out = {"workload": "BASELINE config 5a: levelize the 1M-vertex depends_on DAG (deep chains + wide fan-out, "
+                       "333 3-cycles)", "V": V, "E": E, "value": (V + E) / step_s, "unit": "(V+E)/s",
+           "ms_per_step": step_s * 1e3, "steps": steps, "kernel_ms": kernel_s * 1e3,
+           "levels": int(levels[levels != 0xFFFFFFFF].max()) + 1, "cycle_vertices": int(ncyc_t.item()),
+           "roofline": {"bound": "hbm", "kernel": "levelizer (k_indeg + k_lvl_async + level sort, fp_order.hip)",
+                        "achieved": nbytes / kernel_s / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": nbytes / kernel_s / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                        "algorithmic_bytes": nbytes,
+                        "limiter": "latency of the longest dependency chain (500 levels of chains)"}}
+    return out, (rp, col, hd), level_t, (levels, order_t.cpu().numpy().view(np.uint32), int(ncyc_t.item()))
 
 
 # VALU lane-operations per container x node evaluation in k_feas's inner loop (no bitmap):
@@ -402,17 +550,34 @@ def worker(args):
     if world == 1 and rank == 0:
         del db, pristine
         torch.cuda.empty_cache()
-        if not args.no_config3:
-            out["config3"] = config3_leg(planner, dev, args.config3_steps, 1)
+        gpu = {}  # plans of the single-scenario legs, for the oracle check
+        if not args.no_legs:
+            r, plan = single_leg(planner, dev, "config2", SEED2, C2, N2, FLAGS2, 10, 2)
+            gpu["config2"] = {"plan": plan}
+            out["config2"] = dict({"workload": "BASELINE config 2: 1 scenario x 10k services x 1k servers, "
+                                               "cpu/mem/port constraints"}, **r)
+            r, plan = single_leg(planner, dev, "config3", SEED3, C3, N3, FLAGS, args.config3_steps, 1)
+            gpu["config3"] = {"plan": plan}
+            out["config3"] = dict({"workload": "BASELINE config 3: 1 scenario x 1M containers x 100k nodes, "
+                                               "ports+anti-affinity+labels"}, **r)
+            lv, graph, level_t, levels = levelize_leg(planner, dev, 5)
+            r, plan = single_leg(planner, dev, "config5", SEED5, graph[2].size, N5, FLAGS, args.config3_steps, 1,
+                                 level_t=level_t)
+            gpu["config5"] = {"plan": plan, "graph": graph, "levels": levels}
+            out["config5"] = {"workload": "BASELINE config 5: levelize the 1M-vertex DAG, then place its 1M "
+                                          "containers on 100k nodes (CYCLE members skipped)",
+                              "levelize": lv, "place": r,
+                              "ms_per_step": lv["ms_per_step"] + r["ms_per_step"]}
+            del level_t
+            torch.cuda.empty_cache()
         if not args.no_stage2:
             out["stage2"] = stage2_leg(planner, dev, 3)
         if not args.no_cpu_baseline:
-            try:
-                usable = len(os.sched_getaffinity(0))
-            except AttributeError:
-                usable = os.cpu_count() or 1
-            threads = args.cpu_threads or min(16, usable)
+            usable, quota, avail = _cpu_quota()
+            threads = args.cpu_threads or avail
             out["cpu_baseline"] = cpu_baseline(args.cpu_budget_s, threads)
+            if not args.no_legs:
+                out["cpu_single_thread"] = cpu_single_thread_legs(gpu)
     if out is not None:
         print(json.dumps(out), flush=True)
     planner.close()

@@ -86,7 +86,8 @@ struct PipeArgs {
     uint32_t bounded; // 1: links are rings with back-pressure (every segment co-resident, lag 0)
     uint32_t flush;   // idle flushes of partial output slots: bit 0 LDS rings, bit 1 global links (bounded)
     uint32_t kpack;   // 1: s_idx carries the bucket indices (bits 21-25 cpu, 26-30 mem; C <= 2^21)
-    uint32_t sys;     // systolic group fill for queues of >= sys containers (0: serial loop only)
+    uint32_t sys;     // systolic group fill: queues of >= (sys & 0xFFFF) containers, (sys >> 16) extra
+                      // steps before the serial finish (0: serial loop only)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
     uint32_t *ghead;  // [S][B-1] link control, 256 B apart: [0] head, [32] consumer tail
@@ -247,6 +248,10 @@ using RecT = uint32_t[G];
 #ifndef FP_PF_MAX
 #define FP_PF_MAX 16
 #endif
+// systolic group fill (fp_pipe_sys.h) in stages of at most this many groups
+#ifndef FP_SYS_MAX_G
+#define FP_SYS_MAX_G 4
+#endif
 // the serial loop over one group's queue: the exec-masked loop (fp_pipe_asm.h,
 // fpp_group_x: 172 vs 264 cycles per container in tools/ubench/place.hip); -DFP_GROUP_LOOP=
 // fpp_asm_group selects round 2's readlane / writelane loop for A/B runs
@@ -289,9 +294,10 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
             if (q) {
                 uint64_t touched = 0;
                 // long queues (a filling group): the systolic loop, else the serial one
-                if (sys && (uint32_t)__builtin_popcountll(q) >= sys)
+                // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
+                if (G <= FP_SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
                     fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
-                                         req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
+                                         req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm, sys >> 16);
                 else
                     FPP_GROUP_LOOP<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                          req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
@@ -1341,6 +1347,7 @@ struct PipeGeom {
     uint32_t bounded;   // links are rings with back-pressure
     uint32_t resident;  // workgroups of this kernel resident on the device at once (0: unknown)
     uint32_t sys;       // systolic group fill for queues of >= sys containers (0: off)
+    uint32_t sys_extra; // systolic steps past the queue length before the serial finish
 };
 
 // Global link ring size when every segment of the launch is co-resident: 256 slots x 64
@@ -1405,8 +1412,15 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     g->bounded = (uint32_t)fp_opt(c, FP_OPT_LINK_BOUNDED, (fits && margin && g->lag == 0 && ring < full) ? 1 : 0);
     if (B <= 1) g->bounded = 0;
     g->slots = g->bounded ? (ring < full ? ring : full) : full;
-    // systolic group fill (fp_pipe_sys.h): queues of at least this many containers
-    g->sys = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 0);
+    // systolic group fill (fp_pipe_sys.h): queues of at least this many containers (compiled for
+    // stages of at most FP_SYS_MAX_G groups)
+    // Default: queues of >= 32 containers in the narrow stages (configs 2 / 3 / 5: one scenario,
+    // one-group stages); config 3's k_ffd_pipe 72.1 -> 65.2 ms, config 2 0.81 -> 0.75 ms, every
+    // threshold from 1 to 48 within 1 % (tools/sys_sweep.py, profiles/r03c_sys_sweep.jsonl)
+    g->sys = G <= FP_SYS_MAX_G ? (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 32) : 0u;
+    if (g->sys > 64) g->sys = 64;
+    g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
+    if (g->sys_extra > 128) g->sys_extra = 128;
     return true;
 }
 
@@ -1498,7 +1512,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.cf = b->cpu_free; a.mf = b->mem_free; a.lab = b->labels; a.cu = b->conflict_used; a.sched = b->schedulable;
     a.assign = asg_s; a.reason = rsn_s; a.cost = b->cost; a.err = c->d_err;
     a.spin_ticks = (uint64_t)fp_opt(c, FP_OPT_SPIN_TICKS, (int64_t)SPIN_TICKS);
-    a.sys = geo.sys;
+    a.sys = geo.sys ? (geo.sys | (geo.sys_extra << 16)) : 0u;
     // bucket thresholds (fp_place.hip chooses them; any ascending choice with T0 = 0 is
     // exact -- it only decides how tight the candidate masks are)
     memcpy(a.tc, tc, sizeof(a.tc));

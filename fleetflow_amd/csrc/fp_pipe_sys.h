@@ -144,11 +144,14 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     // later) -> positions 0..L-1, in node order
     const uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
     const uint32_t L = (uint32_t)__builtin_popcountll(lm);
-    const bool inq = (q >> lane) & 1ull;
     if (L == 0) {  // nothing can fit: every queued container misses the group
-        if (inq) asg = 0xFFFFFFFFu;
+        if ((q >> lane) & 1ull) asg = 0xFFFFFFFFu;
         return out;
     }
+    // (A per-call prefilter -- label union, conflict intersection and the largest free cpu /
+    // mem over the live nodes, four wave reductions -- cost more than the misses it dropped:
+    // config 3 65.2 -> 68.7 ms.  Misses end at the step cap and in the serial finish instead.)
+    const bool inq = (q >> lane) & 1ull;
     const uint32_t Q = (uint32_t)__builtin_popcountll(q);
     // containers -> lanes 0..Q-1 (rank among the queued), the others after them
     const uint32_t rq = inq ? (uint32_t)__builtin_popcountll(q & below) : Q + (uint32_t)__builtin_popcountll(~q & below);
@@ -212,11 +215,6 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     return out;
 }
 
-// Steps the systolic phase runs past the queue length before the serial loop takes the
-// containers still open (measured: tools/ubench/systolic.hip)
-#ifndef FP_SYS_EXTRA
-#define FP_SYS_EXTRA 16
-#endif
 
 // Drop-in for fpp_group_x (same arguments): the systolic loop, the serial finish of what it
 // left open, and the same per-group vector epilogue (placed bits of the hits, next candidate
@@ -226,10 +224,12 @@ __device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint
                                               uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
                                               uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
                                               uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
-                                              uint32_t &nhit, uint32_t qc, uint32_t qm) {
+                                              uint32_t &nhit, uint32_t qc, uint32_t qm, uint32_t extra) {
     const uint32_t gbg = gb64 + g * 64u;
+    // `extra`: steps the systolic phase runs past the queue length before the serial loop
+    // takes the containers still open (PipeArgs::sys_extra)
     const SysOut so = fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm,
-                                    (uint32_t)__builtin_popcountll(q) + FP_SYS_EXTRA);
+                                    (uint32_t)__builtin_popcountll(q) + extra);
     uint64_t left = fpp_uniform64(so.left);
     touched = fpp_uniform64(touched);
     if (left) fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);

@@ -21,15 +21,23 @@
  *   - All buffers are caller-owned; no allocation crosses the ABI.
  *   - fp_* take HOST pointers and are synchronous: on error nothing is written.
  *   - fp_dev_* take DEVICE (HBM) pointers of the context's device and are
- *     asynchronous on the context's stream.  Kernel-side errors (FP_ECORRUPT input,
- *     FP_EDEVICE from the placement pipeline's deadlock guard) are sticky: the first
- *     one raised is kept until fp_ctx_sync() -- or the next host-pointer call, or the
- *     levelizer's own mid-call check -- reports it and clears it.
+ *     asynchronous on the context's stream.  Kernel-side errors of fp_dev_* calls
+ *     (FP_ECORRUPT input, FP_EDEVICE from the placement pipeline's deadlock guard) are
+ *     sticky: the first one raised is kept until fp_ctx_sync() (or fp_dev_levelize's own
+ *     mid-call check) reports it and clears it.  A host-pointer call reports only the
+ *     errors of its own kernels (it has its own error word): a pending asynchronous error
+ *     neither fails it nor is cleared by it.
  *     fp_dev_place_batch and fp_dev_levelize read a few words back to size their
  *     sort keys / level count, so they synchronise the stream once or twice per call;
  *     their kernels stay queued and asynchronous.
- *   - fp_ctx_set_stream drains the old stream before switching (the device
- *     workspace is reused by every call).
+ *   - fp_ctx_set_stream first waits for the context's last fp_dev_* call (an event
+ *     recorded on the old stream; the workspace is reused by every call).  It never
+ *     touches the old stream handle itself, so a caller may destroy that stream once
+ *     its own work on it is done.
+ *   - The placement pipeline's bounded links (fp_place_geometry FP_GEOM_BOUNDED) assume
+ *     the launch gets at least half of the device's resident workgroup slots; work of
+ *     other processes crowding it out beyond that ends in FP_EDEVICE after the deadlock
+ *     guard (60 s), never in a wrong plan.
  *   - Return 0 (FP_OK) or a negative FP_E* code.  There is no CPU fallback:
  *     fp_ctx_create fails with FP_EDEVICE when no MI355X (gfx950) is present.
  *   - One fp_ctx per host thread; contexts are not shared.
@@ -128,8 +136,9 @@ int fp_ctx_kernel_stats(fp_ctx *ctx, int kernel_id, double *total_ms, uint64_t *
  * only the context it is set on.  The pipeline geometry options are hints a shape may
  * not be able to serve (the planner then falls back to the nearest valid geometry);
  * fp_place_geometry reports what a call will run.  Results are bit-exact whatever the
- * options (only the work schedule changes), except FP_OPT_SPIN_TICKS, which can make a
- * call fail with FP_EDEVICE. */
+ * options (only the work schedule changes); FP_OPT_SPIN_TICKS, and FP_OPT_LINK_BOUNDED = 1
+ * on a batch whose segments are not all resident, can make a call fail with FP_EDEVICE
+ * (never a wrong plan). */
 #define FP_OPT_AUTO (-1)
 enum fp_option {
     FP_OPT_PIPE_W = 0,        /* stages (waves) per segment, >= 1                         */
@@ -145,7 +154,8 @@ enum fp_option {
     FP_OPT_SEGSORT = 10,      /* 0 = device-wide radix sort instead of segmented            */
     FP_OPT_SYSTOLIC = 11,     /* systolic group fill for queues of >= value containers (0 = off) */
     FP_OPT_LEVELIZE_SYNC = 12,/* 1 = level-synchronous Kahn instead of the async levelizer */
-    FP_OPT_COUNT = 13
+    FP_OPT_SYSTOLIC_EXTRA = 13, /* systolic steps past the queue length before the serial finish */
+    FP_OPT_COUNT = 14
 };
 int fp_ctx_set_option(fp_ctx *ctx, int option, int64_t value);
 int fp_ctx_get_option(fp_ctx *ctx, int option, int64_t *value);

@@ -6,12 +6,19 @@
 //!   for the call at engine.rs:157;
 //! * [`start_levels`] / [`start_waves`] -- Kahn start levels, the parallel start waves for
 //!   `DeployEngine::create_and_start` (engine.rs:355-452);
-//! * [`resolve_target_server`] / [`Planner::place`] -- the server choice of
-//!   crates/fleetflow-controlplane/src/handlers/deploy.rs:390-398 (`servers.first()`), and the
-//!   first-fit-decreasing fan-out that replaces it.
+//! * [`resolve_target_server`] -- the server choice of
+//!   crates/fleetflow-controlplane/src/handlers/deploy.rs:390-398 (`servers.first()`), exactly
+//!   as the reference computes it (no planning involved, no GPU needed), and
+//!   [`Planner::place`] / [`place_stage`] -- the first-fit-decreasing fan-out that replaces it
+//!   when server capacity matters;
+//! * [`plan_scenarios`] / [`Planner::place_batch`] -- what-if planning: many independent
+//!   scenarios in one call, a packed cost per scenario and the best plan, the single-host
+//!   counterpart of the controlplane routing a deploy to one target (deploy.rs:441-451).
 //!
 //! Strings never cross the ABI: names map to u32 ids in stage order here.  There is no CPU
-//! fallback: without an MI355X every call returns [`PlanError`] (FP_EDEVICE).
+//! fallback for the planning calls: without an MI355X they return [`PlanError`] (FP_EDEVICE),
+//! and [`order_by_dependencies`] panics like any use of the crate on a host without the GPU
+//! it is built for.
 pub mod ffi;
 
 use fleetflow_core::Flow;
@@ -92,6 +99,74 @@ impl Planner {
     }
 }
 
+impl Planner {
+    /// What-if planning over `b.n_scen` independent scenarios (fleetplace.h `fp_place_batch`):
+    /// every scenario's plan, its packed cost `(n_rejected:24 | n_nodes_used:24 | id:16)` and
+    /// the updated node tables, in `b` (scenario-major arrays).
+    pub fn place_batch(&mut self, b: &mut Batch) -> Result<(), PlanError> {
+        let (s, c, n) = (b.n_scen as usize, b.n_containers as usize, b.n_nodes as usize);
+        let ok = b.containers.cpu_m.len() == s * c && b.nodes.cpu_free.len() == s * n
+            && b.level.as_ref().map_or(true, |l| l.len() == s * c);
+        if !ok {
+            return Err(PlanError(ffi::FP_EINVAL));
+        }
+        b.assign.resize(s * c, 0);
+        b.reason.resize(s * c, 0);
+        b.cost.resize(s, 0);
+        let fb = ffi::fp_batch {
+            n_scen: b.n_scen, scen_base: b.scen_base, n_containers: b.n_containers, n_nodes: b.n_nodes,
+            cpu_m: b.containers.cpu_m.as_ptr(), mem_mib: b.containers.mem_mib.as_ptr(),
+            req_labels: b.containers.req_labels.as_ptr(), conflict: b.containers.conflict.as_ptr(),
+            level: b.level.as_ref().map_or(std::ptr::null(), |l| l.as_ptr()),
+            cpu_free: b.nodes.cpu_free.as_mut_ptr(), mem_free: b.nodes.mem_free.as_mut_ptr(),
+            labels: b.nodes.labels.as_ptr(), conflict_used: b.nodes.conflict_used.as_mut_ptr(),
+            schedulable: b.nodes.schedulable.as_ptr(), assign: b.assign.as_mut_ptr(), reason: b.reason.as_mut_ptr(),
+            cost: b.cost.as_mut_ptr(),
+        };
+        check(unsafe { ffi::fp_place_batch(self.ctx, &fb) })
+    }
+
+    /// The same planning on HBM-resident arrays (fleetplace.h `fp_dev_place_batch`, asynchronous
+    /// on the context's stream), then the best scenario on the device
+    /// (`fp_dev_argmin_cost` into `best_dev`).  Kernel errors surface at [`Planner::sync`].
+    ///
+    /// # Safety
+    /// Every pointer in `b` and `best_dev` must be device memory of this context's GPU, sized as
+    /// fleetplace.h documents, and stay valid until the stream has drained.
+    pub unsafe fn dev_place_batch(&mut self, b: &ffi::fp_batch, best_dev: *mut u32) -> Result<(), PlanError> {
+        check(ffi::fp_dev_place_batch(self.ctx, b))?;
+        if !b.cost.is_null() && !best_dev.is_null() && b.n_scen > 0 {
+            check(ffi::fp_dev_argmin_cost(self.ctx, b.cost, b.n_scen, best_dev))?;
+        }
+        Ok(())
+    }
+
+    /// Waits for the context's asynchronous calls and reports their first kernel error.
+    pub fn sync(&mut self) -> Result<(), PlanError> {
+        check(unsafe { ffi::fp_ctx_sync(self.ctx) })
+    }
+
+    /// Device workspace a batch of this shape takes (grown once per context, then reused).
+    pub fn workspace_bytes(&mut self, n_scen: u32, n_containers: u32, n_nodes: u32) -> Result<u64, PlanError> {
+        let mut bytes = 0u64;
+        check(unsafe { ffi::fp_place_ws_bytes(self.ctx, n_scen, n_containers, n_nodes, &mut bytes) })?;
+        Ok(bytes)
+    }
+
+    /// The placement pipeline a batch of this shape runs (`FP_GEOM_*` indices).
+    pub fn geometry(&mut self, n_scen: u32, n_containers: u32, n_nodes: u32)
+                    -> Result<[u32; ffi::FP_GEOM_COUNT], PlanError> {
+        let mut out = [0u32; ffi::FP_GEOM_COUNT];
+        check(unsafe { ffi::fp_place_geometry(self.ctx, n_scen, n_containers, n_nodes, out.as_mut_ptr()) })?;
+        Ok(out)
+    }
+
+    /// A per-context option (`FP_OPT_*`; `FP_OPT_AUTO` restores the default).
+    pub fn set_option(&mut self, option: i32, value: i64) -> Result<(), PlanError> {
+        check(unsafe { ffi::fp_ctx_set_option(self.ctx, option, value) })
+    }
+}
+
 impl Drop for Planner {
     fn drop(&mut self) {
         unsafe { ffi::fp_ctx_destroy(self.ctx) }
@@ -115,6 +190,47 @@ pub struct Nodes {
     pub labels: Vec<u32>,
     pub conflict_used: Vec<u32>,
     pub schedulable: Vec<u8>,
+}
+
+/// `n_scen` independent what-if scenarios of `n_containers` x `n_nodes`, scenario-major
+/// (`containers.*[s * C + i]`, `nodes.*[s * N + j]`); outputs filled by [`Planner::place_batch`].
+pub struct Batch {
+    pub n_scen: u32,
+    /// global id of scenario 0 in the packed costs (scen_base + n_scen <= 65536)
+    pub scen_base: u32,
+    pub n_containers: u32,
+    pub n_nodes: u32,
+    pub containers: Containers,
+    pub nodes: Nodes,
+    /// start levels ([S * C]); `FP_NONE` marks a CYCLE member, which is not placed
+    pub level: Option<Vec<u32>>,
+    pub assign: Vec<u32>,
+    pub reason: Vec<u8>,
+    pub cost: Vec<u64>,
+}
+
+/// The outcome of [`plan_scenarios`]: every scenario's packed cost, the best scenario (lowest
+/// cost; the id field breaks ties towards the lowest id) and its plan.
+pub struct ScenarioPlans {
+    pub cost: Vec<u64>,
+    pub best: u32,
+    pub assign: Vec<u32>,
+    pub reason: Vec<u8>,
+}
+
+/// Unpacks a packed scenario cost: (rejected containers, nodes used, scenario id).
+pub fn unpack_cost(c: u64) -> (u32, u32, u32) {
+    ((c >> 40) as u32, ((c >> 16) & 0xFF_FFFF) as u32, (c & 0xFFFF) as u32)
+}
+
+/// Plans every scenario of `b` on this thread's GPU and picks the best one (the what-if
+/// surface of the controlplane: one target per deploy, deploy.rs:441-451).
+pub fn plan_scenarios(b: &mut Batch) -> Result<ScenarioPlans, PlanError> {
+    with_planner(|p| p.place_batch(b))?;
+    let c = b.n_containers as usize;
+    let best = b.cost.iter().enumerate().min_by_key(|&(i, &v)| (v, i)).map_or(0, |(i, _)| i);
+    Ok(ScenarioPlans { cost: b.cost.clone(), best: best as u32, assign: b.assign[best * c..(best + 1) * c].to_vec(),
+                       reason: b.reason[best * c..(best + 1) * c].to_vec() })
 }
 
 thread_local! {
@@ -225,22 +341,27 @@ pub fn start_waves(services: &[String], flow: &Flow) -> Result<(Vec<Vec<String>>
     Ok((by_level.into_values().collect(), cycle))
 }
 
-/// crates/fleetflow-controlplane/src/handlers/deploy.rs:390-394:
-/// `flow.stages.get(stage).and_then(|s| s.servers.first().cloned())`, computed as FFD over the
-/// stage's servers with unconstrained capacity (every service lands on node 0).  `None` means
-/// the caller's "local" fallback (:396-398).
-pub fn resolve_target_server(flow: &Flow, stage_name: &str) -> Result<Option<String>, PlanError> {
-    let Some(stage) = flow.stages.get(stage_name) else { return Ok(None) };
-    if stage.servers.is_empty() {
-        return Ok(None);
+/// crates/fleetflow-controlplane/src/handlers/deploy.rs:390-394, as the reference computes it:
+/// `flow.stages.get(stage).and_then(|s| s.servers.first().cloned())`.  `None` means the caller's
+/// "local" fallback (:396-398).  Pure Rust: choosing the first declared server needs no planner
+/// (and so no GPU); [`place_stage`] is the capacity-aware fan-out that replaces it.
+pub fn resolve_target_server(flow: &Flow, stage_name: &str) -> Option<String> {
+    flow.stages.get(stage_name).and_then(|s| s.servers.first().cloned())
+}
+
+/// Per-service server choice for a stage (the fan-out deploy.rs:388-389 leaves for later):
+/// first-fit-decreasing of the stage's services (requests in `c`, stage order) over its servers
+/// (`nodes`, `stage.servers` order), on the GPU.  Returns the server of every service, `None`
+/// for one that fits nowhere (NOFIT).  With unconstrained capacity every service lands on the
+/// first server, i.e. [`resolve_target_server`].
+pub fn place_stage(flow: &Flow, stage_name: &str, c: &Containers, nodes: &mut Nodes)
+                   -> Result<Vec<Option<String>>, PlanError> {
+    let Some(stage) = flow.stages.get(stage_name) else { return Err(PlanError(ffi::FP_EINVAL)) };
+    if nodes.cpu_free.len() != stage.servers.len() || c.cpu_m.len() != stage.services.len() {
+        return Err(PlanError(ffi::FP_EINVAL));
     }
-    let n = stage.services.len().max(1);
-    let k = stage.servers.len();
-    let c = Containers { cpu_m: vec![0; n], mem_mib: vec![0; n], req_labels: vec![0; n], conflict: vec![0; n] };
-    let mut nodes = Nodes { cpu_free: vec![u32::MAX; k], mem_free: vec![u32::MAX; k], labels: vec![0; k],
-                            conflict_used: vec![0; k], schedulable: vec![1; k] };
-    let (assign, _) = with_planner(|p| p.place(&c, &mut nodes, None))?;
-    Ok(Some(stage.servers[assign[0] as usize].clone()))
+    let (assign, _) = with_planner(|p| p.place(c, nodes, None))?;
+    Ok(assign.iter().map(|&a| if a == ffi::FP_NONE { None } else { Some(stage.servers[a as usize].clone()) }).collect())
 }
 
 #[cfg(all(test, feature = "gpu-tests"))]
@@ -279,6 +400,22 @@ mod tests {
         let f = flow(&[("api", &["db"]), ("db", &[]), ("redis", &[]), ("worker", &["redis", "db"])]);
         let out = order_by_dependencies(&names(&["api", "db", "redis", "worker"]), &f);
         assert_eq!(out, names(&["db", "redis", "api", "worker"]));
+    }
+
+    #[test]
+    fn scenarios_pick_the_cheapest_plan() {
+        // two scenarios of two containers on one node: scenario 1's node is too small for
+        // one of them, so scenario 0 (nothing rejected) is the best plan
+        let c = Containers { cpu_m: vec![500, 500, 500, 500], mem_mib: vec![64; 4], req_labels: vec![0; 4],
+                             conflict: vec![0; 4] };
+        let nodes = Nodes { cpu_free: vec![1000, 600], mem_free: vec![1024, 1024], labels: vec![0; 2],
+                            conflict_used: vec![0; 2], schedulable: vec![1; 2] };
+        let mut b = Batch { n_scen: 2, scen_base: 0, n_containers: 2, n_nodes: 1, containers: c, nodes, level: None,
+                            assign: vec![], reason: vec![], cost: vec![] };
+        let p = plan_scenarios(&mut b).unwrap();
+        assert_eq!(p.best, 0);
+        assert_eq!(unpack_cost(p.cost[1]), (1, 1, 1));
+        assert_eq!(p.assign, vec![0, 0]);
     }
 
     #[test]

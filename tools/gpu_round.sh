@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session: error-path tests (isolated, short limit), the -m gpu suite, the bench
 # (config 4 at 4096 + config 3 leg + CPU baseline), then the rocprofv3 passes.
-# Usage: tools/gpu_round.sh <tag> [steps...]   steps: errors tests bench prof (default: all)
+# Usage: tools/gpu_round.sh <tag> [steps...]   steps: errors tests bench scale prof (default: errors tests bench prof)
 set -o pipefail
 tag=${1:?tag}; shift
 steps=${*:-errors tests bench prof}
@@ -22,6 +22,12 @@ for s in $steps; do
       timeout -k 10 400 python -u bench.py > ${log}_bench.json 2> ${log}_bench.err \
         || { echo "bench failed"; tail -30 ${log}_bench.err; exit 1; }
       cat ${log}_bench.json ;;
+    scale)
+      # per-rank loads of the strong-scaled config 4 (4096 / N scenarios on one GPU)
+      for sc in 2048 1024 512; do
+        timeout -k 10 200 python -u bench.py --scenarios $sc --no-legs --no-stage2 --no-cpu-baseline --steps 10 \
+          > ${log}_scale_$sc.json 2> ${log}_scale_$sc.err || { echo "scale $sc failed"; tail -20 ${log}_scale_$sc.err; exit 1; }
+      done ;;
     prof)
       timeout -k 10 1000 bash tools/profile.sh $tag || { echo "profile failed"; exit 1; } ;;
     stats)

@@ -8,7 +8,7 @@ out=$root/gpurun_out/kt_$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- \
-  python3 "$root/bench.py" --no-cpu-baseline --no-config3 --no-stage2 --steps 2 --warmup 1 "$@" > "$out/log.txt" 2>&1
+  python3 "$root/bench.py" --no-cpu-baseline --no-legs --no-stage2 --steps 2 --warmup 1 "$@" > "$out/log.txt" 2>&1
 f=$(find "$out" -name '*kernel_stats.csv' | head -1)
 python3 - "$f" <<'PY'
 import csv, sys

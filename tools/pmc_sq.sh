@@ -7,7 +7,7 @@ root=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$root/gpurun_out/sq_$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
-args="$root/bench.py --no-cpu-baseline --no-config3 --no-stage2 --steps 2 --warmup 1"
+args="$root/bench.py --no-cpu-baseline --no-legs --no-stage2 --steps 2 --warmup 1"
 i=0
 for pmc in "SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "SQ_WAIT_ANY SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_INSTS SQ_IFETCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \

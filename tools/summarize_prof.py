@@ -5,9 +5,8 @@ merges gpurun_out/).  Writes
   profiles/<tag>_pmc.json           per-leg k_ffd_pipe duration + PMC bytes
   profiles/pmc_latest.json          the same, read by bench.py's roofline
 
-The bench launches k_ffd_pipe for two legs with different grids: config 4 (4096
-scenarios: the largest grid) and config 3 (one 1M x 100k scenario).  Dispatches are
-grouped by grid size; the largest grid is config 4, the next config 3.
+The bench launches k_ffd_pipe for four legs (by_leg below tells them apart by grid size and
+dispatch order): config 4 (4096 scenarios), config 2, config 3 and config 5b.
 HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half the bytes of
 wide coalesced reads, MI355X_MICROARCH.md "HBM"), each counter from its own --pmc pass."""
 import csv
@@ -20,7 +19,13 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "k_ffd_pipe"
-LEGS = [("config4", 4096, 50_000, 5_000), ("config3", 1, 1_000_000, 100_000)]
+# bench.py's k_ffd_pipe launches per leg, in run order (tools/profile.sh: --steps 2 --warmup 1
+# --config3-steps 1): config 4 (warmup + steps), config 2 (2 + 10), config 3 (1 + 1), config 5b
+# (1 + 1).  Configs 3 and 5b have the same grid (391 segments of 4 stages): they are told apart
+# by dispatch order, config 3's launches coming first.
+LEGS = [("config4", 4096, 50_000, 5_000), ("config2", 1, 10_000, 1_000), ("config3", 1, 1_000_000, 100_000),
+        ("config5", 1, 1_000_000, 100_000)]
+N_CONFIG3 = 2
 
 
 def rows(pattern):
@@ -31,12 +36,25 @@ def rows(pattern):
     return out
 
 
-def by_grid(rs, grid_key):
+def by_leg(rs, grid_key):
+    """k_ffd_pipe rows per leg: the largest grid is config 4, the smallest config 2, the
+    remaining grid holds config 3 then config 5b in dispatch order."""
     g = {}
     for r in rs:
         if KERNEL in r["Kernel_Name"]:
             g.setdefault(int(r[grid_key]), []).append(r)
-    return [g[k] for k in sorted(g, reverse=True)]
+    grids = sorted(g, reverse=True)
+    out = {}
+    if not grids:
+        return out
+    out["config4"] = g[grids[0]]
+    if len(grids) >= 3:
+        out["config2"] = g[grids[-1]]
+        mid = sorted(g[grids[1]], key=lambda r: int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0))
+        out["config3"], out["config5"] = mid[:N_CONFIG3], mid[N_CONFIG3:]
+    elif len(grids) == 2:
+        out["config3"] = g[grids[1]]
+    return out
 
 
 def main():
@@ -46,21 +64,22 @@ def main():
     if not stats:
         sys.exit(f"no kernel_stats.csv under {base}/trace")
     shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
-    trace = by_grid(rows(os.path.join(base, "trace", "**", "*kernel_trace.csv")), "Grid_Size_X")
-    fetch = by_grid([r for r in rows(os.path.join(base, "fetch", "**", "*counter_collection.csv"))
-                     if r["Counter_Name"] == "FETCH_SIZE"], "Grid_Size")
-    write = by_grid([r for r in rows(os.path.join(base, "write", "**", "*counter_collection.csv"))
-                     if r["Counter_Name"] == "WRITE_SIZE"], "Grid_Size")
+    trace = by_leg(rows(os.path.join(base, "trace", "**", "*kernel_trace.csv")), "Grid_Size_X")
+    fetch = by_leg([r for r in rows(os.path.join(base, "fetch", "**", "*counter_collection.csv"))
+                    if r["Counter_Name"] == "FETCH_SIZE"], "Grid_Size")
+    write = by_leg([r for r in rows(os.path.join(base, "write", "**", "*counter_collection.csv"))
+                    if r["Counter_Name"] == "WRITE_SIZE"], "Grid_Size")
     out = {}
-    for i, (leg, S, C, N) in enumerate(LEGS):
-        if i >= len(trace):
-            break
-        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace[i]]
-        f = statistics.mean(float(r["Counter_Value"]) for r in fetch[i]) if i < len(fetch) else None
-        w = statistics.mean(float(r["Counter_Value"]) for r in write[i]) if i < len(write) else None
+    for leg, S, C, N in LEGS:
+        tr = trace.get(leg)
+        if not tr:
+            continue
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
+        f = statistics.mean(float(r["Counter_Value"]) for r in fetch[leg]) if fetch.get(leg) else None
+        w = statistics.mean(float(r["Counter_Value"]) for r in write[leg]) if write.get(leg) else None
         out[leg] = {
             "kernel": KERNEL, "tag": tag, "S": S, "C": C, "N": N,
-            "grid_threads": int(trace[i][0]["Grid_Size_X"]),
+            "grid_threads": int(tr[0]["Grid_Size_X"]),
             "launches_traced": len(durs),
             "avg_duration_ms": statistics.mean(durs) / 1e6,
             "fetch_size_kb": f, "write_size_kb": w,
