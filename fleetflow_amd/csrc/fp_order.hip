@@ -202,6 +202,21 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 
 // Sources (in-degree 0) with out-edges go to the queues; every other vertex starts
 // at level NONE (a source without out-edges is final here).
+// One 16-B record per CSR edge: the child, the child's own edge range, and whether this edge
+// is the child's only in-edge.  A chain hop then costs one load round trip: the record of the
+// continuation's first edge names the next vertex AND where its edges are, and a child whose
+// only parent is the expanding vertex is ready without an atomic (its level is the parent's
+// + 1 >= has_deps; nothing else ever touches its state word).  Round 2 paid three: col[e],
+// then row_ptr[w] beside the CAS on state[w], then the next col.
+__global__ void k_edge_rec(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t E,
+                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec) {
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t w = col[e];
+        rec[e] = w < V ? make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u)
+                       : make_uint4(w, 0u, 0u, 0u);  // corrupt: k_indeg raised FP_ECORRUPT, no expansion runs
+    }
+}
+
 __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
                                  const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t *__restrict__ level,
                                  uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
@@ -230,7 +245,7 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
             ((uint64_t)(pk ? l0 << 8 : l0) << 32) | v;
 }
 
-__global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
+__global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
                                                   uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
                                                   uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
                                                   uint32_t *__restrict__ err, bool pk) {
@@ -280,8 +295,11 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                 uint32_t ww = 0;
                 uint64_t cur = 0;
                 if (ee < be1) {
-                    ww = col[ee];
+                    const uint4 er = erec[ee];
+                    ww = er.x;
                     uint64_t exp = (1ull << 32) | 1ull;
+                    if (er.w) cur = (uint64_t)(blu + 1u) << 32;  // the only parent: ready, no atomic
+                    else
                     while (true) {
                         const uint32_t nl = max((uint32_t)(exp >> 32), blu + 1u);
                         const uint64_t nv = ((uint64_t)nl << 32) | (uint32_t)((uint32_t)exp - 1u);
@@ -322,12 +340,13 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             const uint32_t ne = min(e1 - e, kLaneEdges);
             uint32_t p0[kLaneEdges], p1[kLaneEdges];
             uint64_t cur[kLaneEdges], obs[kLaneEdges];
+            bool only[kLaneEdges];
 #pragma unroll
             for (uint32_t k = 0; k < kLaneEdges; ++k)
-                if (k < ne) w[k] = col[e + k];
-#pragma unroll
-            for (uint32_t k = 0; k < kLaneEdges; ++k)
-                if (k < ne) { p0[k] = row_ptr[w[k]]; p1[k] = row_ptr[w[k] + 1]; }  // speculative continuation edges
+                if (k < ne) {  // the child and its edge range (the continuation's) in one record
+                    const uint4 er = erec[e + k];
+                    w[k] = er.x; p0[k] = er.y; p1[k] = er.z; only[k] = er.w != 0u;
+                }
             // first attempt guesses an untouched vertex with deps and one parent (a chain link)
             const uint64_t g = (1ull << 32) | 1ull;
             const uint64_t gn = ((uint64_t)max(1u, lu + 1u) << 32);
@@ -335,9 +354,10 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             for (uint32_t k = 0; k < kLaneEdges; ++k) {
                 if (k < ne) {
                     obs[k] = g;
-                    cur[k] = __hip_atomic_compare_exchange_strong(&state[w[k]], &obs[k], gn, __ATOMIC_RELAXED,
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 ? gn : kQEmpty;
+                    cur[k] = only[k] ? gn  // this edge is the child's only in-edge: ready, no atomic
+                                     : __hip_atomic_compare_exchange_strong(&state[w[k]], &obs[k], gn, __ATOMIC_RELAXED,
+                                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           ? gn : kQEmpty;
                 }
             }
 #pragma unroll
@@ -538,7 +558,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     // cnt[L] = frontier size of level L (one counter per possible level: <= V + 1)
     const size_t ncnt = (size_t)V + 2;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + (size_t)V * 8 * (1 + kShards) +
-                                   kCtlWords * 4 + 20 * 256);
+                                   (size_t)E * 16 + kCtlWords * 4 + 21 * 256);
     if (rc) return rc;
     fp_ws_reset(c);
     uint32_t *indeg = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
@@ -571,7 +591,8 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         uint64_t *state = (uint64_t *)fp_ws_take(c, (size_t)V * 8);
         uint64_t *Q = (uint64_t *)fp_ws_take(c, (size_t)V * 8 * kShards);
         uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
-        if (!state || !Q || !actl) return FP_ENOMEM;
+        uint4 *erec = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
+        if (!state || !Q || !actl || (E && !erec)) return FP_ENOMEM;
         FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
         FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
         // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
@@ -582,8 +603,11 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         // a corrupt CSR (k_check_csr / k_indeg) stops here, before any expansion
         if ((rc = fp_take_err(c))) return rc;
         if (E) {
+            k_edge_rec<<<blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192, 256, 0, st>>>(g->row_ptr, g->col, E, V,
+                                                                                            indeg, erec);
+            FP_HIP(hipGetLastError());
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
-            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, g->col, V, state, Q, actl, level, c->d_err, pk);
+            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, V, state, Q, actl, level, c->d_err, pk);
             FP_HIP(hipGetLastError());
         }
         FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &actl[26 * kCtlStride], 4, hipMemcpyDeviceToHost, st));

@@ -65,6 +65,8 @@ namespace fpp {
 constexpr int K = 32;               // threshold buckets per dimension
 static_assert(K == FP_BUCKETS, "fp_place.hip and the pipeline agree on the bucket count");
 constexpr uint32_t END = 0x80000000u;
+// s_idx bit 31: the container never enters the pipeline (segment 0 writes assign FP_NONE and the
+// reason code its s_req word carries: CYCLE, or NOFIT from the stage-2 screen, k_node_summary)
 constexpr uint32_t CYC = 0x80000000u;
 // Deadlock guard: a wait longer than this (s_memrealtime runs at 100 MHz) aborts the
 // launch with FP_EDEVICE.  Downstream stages legitimately wait for most of a long
@@ -93,7 +95,7 @@ struct PipeArgs {
     uint32_t *ghead;  // [S][B-1] link control, 256 B apart: [0] head, [32] consumer tail
     uint32_t *gdata;  // [S][B-1][slots][2][64] link slots: row 0 = count, row 1 = FFD positions
     uint32_t *part;   // [S][B][2] per-segment (n_used, n_rej)
-    const uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;  // FFD-sorted SoA [S][C]; idx bit31 = CYCLE
+    const uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;  // FFD-sorted SoA [S][C]; idx bit31 = skip
     uint32_t *cf, *mf;
     const uint32_t *lab;
     uint32_t *cu;
@@ -547,10 +549,10 @@ k_ffd_pipe(const PipeArgs a) {
                 idx = a.s_idx[cb + i];
             }
             const bool cyc = valid && (idx & CYC);
-            if (cyc) {
+            if (cyc) {  // CYCLE member, or screened out by stage 2 (NOFIT): s_req holds the reason
                 const uint32_t j = idx & pmask;
                 a.assign[cb + j] = FP_NONE;
-                a.reason[cb + j] = FP_REASON_CYCLE;
+                a.reason[cb + j] = (uint8_t)req;
             }
             n_rej += (uint32_t)__popcll(__ballot(cyc));
             valid = valid && !cyc;
@@ -1035,6 +1037,45 @@ __global__ void k_cost_reduce(uint32_t S, uint32_t B, uint32_t scen_base, const 
 // without keys (all-zero or all-equal demands) everything is.
 // The buckets of both demands (one binary search over the thresholds, in LDS) ride in the
 // position word when positions fit 21 bits (PipeArgs::kpack).
+// ---- stage 2 on the pristine node table, as an exact early NOFIT screen ----
+// Per scenario, the feasibility sweep (SPEC.md 2.3) against one summary record that dominates
+// every schedulable node: the union of their labels and the intersection of their used
+// conflict bits.  A container whose required labels are outside the union, or whose conflict
+// bits every node has already used, has no feasible node now (feasible count 0, fp_feasibility)
+// and none later (capacity and free conflicts only shrink, SPEC.md 2.3 monotonicity): it is
+// NOFIT without entering the pipeline, exactly as the sequential first fit would reject it at
+// the last node.  In the synthetic configs 3 and 4 that is every container requiring one of the
+// 19 label bits no node carries (~18 %): each of them used to walk every segment.
+__global__ __launch_bounds__(256) void k_node_summary(uint32_t N, const uint32_t *__restrict__ lab,
+                                                      const uint32_t *__restrict__ cu,
+                                                      const uint8_t *__restrict__ sched, uint32_t *__restrict__ summ) {
+    const size_t nb = (size_t)blockIdx.x * N;
+    uint32_t u = 0, a = 0xFFFFFFFFu;
+    for (uint32_t n = threadIdx.x; n < N; n += blockDim.x) {
+        if (sched[nb + n]) {
+            u |= lab[nb + n];
+            a &= cu[nb + n];
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        u |= (uint32_t)__shfl_xor((int)u, o);
+        a &= (uint32_t)__shfl_xor((int)a, o);
+    }
+    __shared__ uint32_t red[2][4];
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = u; red[1][w] = a; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t q = 1; q < blockDim.x / 64; ++q) { u |= red[0][q]; a &= red[1][q]; }
+        summ[(size_t)blockIdx.x * 4] = u;
+        summ[(size_t)blockIdx.x * 4 + 1] = a;
+    }
+}
+
+__device__ __forceinline__ bool screened(const uint32_t *sm, uint32_t req, uint32_t conf) {
+    return ((req & ~sm[0]) | (conf & sm[1])) != 0u;
+}
+
 // bucket thresholds for k_gather_sorted (by value: [0, K) cpu, [K, 2K) mem)
 struct GatherThr {
     uint32_t t[2 * K];
@@ -1047,9 +1088,10 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
                                 const uint32_t *__restrict__ cval, const uint32_t *__restrict__ mval,
                                 const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
                                 const uint32_t *__restrict__ req, const uint32_t *__restrict__ conf,
-                                const uint32_t *__restrict__ level, uint32_t *__restrict__ s_cpu,
-                                uint32_t *__restrict__ s_mem, uint32_t *__restrict__ s_req,
-                                uint32_t *__restrict__ s_conf, uint32_t *__restrict__ s_idx) {
+                                const uint32_t *__restrict__ level, const uint32_t *__restrict__ summ,
+                                uint32_t *__restrict__ s_cpu, uint32_t *__restrict__ s_mem,
+                                uint32_t *__restrict__ s_req, uint32_t *__restrict__ s_conf,
+                                uint32_t *__restrict__ s_idx) {
     // S * C < 2^32 (fp_dev_place_batch_impl checks): 32-bit index arithmetic, and four
     // independent elements per thread in flight (the req/conf gathers are dependent loads)
     const uint32_t total = S * C;
@@ -1096,6 +1138,12 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
                 r[u] = req[src[u]];
                 f[u] = conf[src[u]];
                 cy[u] = (level && level[src[u]] == FP_NONE) ? CYC : 0u;
+                if (cy[u]) {
+                    r[u] = FP_REASON_CYCLE;
+                } else if (summ && screened(summ + (size_t)((uint32_t)i / C) * 4, r[u], f[u])) {
+                    cy[u] = CYC;
+                    r[u] = FP_REASON_NOFIT;
+                }
                 if (skeys) {
                     if (cval) cv[u] = cval[cv[u]];
                     if (mval) mv[u] = mval[mv[u]];
@@ -1130,8 +1178,9 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
 // 1.68 ms, but k_digits 0.39 -> 1.05 ms.)
 __global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
                                  const uint32_t *__restrict__ req, const uint32_t *__restrict__ conf,
-                                 const uint32_t *__restrict__ level, uint32_t *__restrict__ s_req,
-                                 uint32_t *__restrict__ s_conf, uint32_t *__restrict__ s_idx) {
+                                 const uint32_t *__restrict__ level, const uint32_t *__restrict__ summ,
+                                 uint32_t *__restrict__ s_req, uint32_t *__restrict__ s_conf,
+                                 uint32_t *__restrict__ s_idx) {
     const uint32_t total = S * C;
     const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t i0 = lb * 4 * blockDim.x + threadIdx.x;
@@ -1148,6 +1197,12 @@ __global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restr
             r[u] = req[src[u]];
             f[u] = conf[src[u]];
             cy[u] = (level && level[src[u]] == FP_NONE) ? CYC : 0u;
+            if (cy[u]) {
+                r[u] = FP_REASON_CYCLE;
+            } else if (summ && screened(summ + (size_t)(i / C) * 4, r[u], f[u])) {
+                cy[u] = CYC;
+                r[u] = FP_REASON_NOFIT;
+            }
         }
     }
 #pragma unroll
@@ -1156,7 +1211,7 @@ __global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restr
         if (i < total) {
             __builtin_nontemporal_store(r[u], &s_req[i]);
             __builtin_nontemporal_store(f[u], &s_conf[i]);
-            if (level && cy[u]) s_idx[i] |= CYC;
+            if (cy[u]) s_idx[i] |= CYC;
         }
     }
 }
@@ -1430,7 +1485,7 @@ size_t fp_pipe_ws_bytes(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N) {
     if (!pipe_geom(c, S, C, N, &g)) return 0;
     const size_t SC = (size_t)S * C, nlinks = (size_t)S * (g.B - 1);
     return 5 * SC * 4 + SC * 5 + 256 + nlinks * LCTL * 4 + (size_t)S * g.B * 8 + 8 + nlinks * g.slots * 2 * 64 * 4 +
-           10 * 256;
+           (size_t)S * 16 + 11 * 256;
 }
 
 uint32_t fp_pipe_kpack(const fp_ctx *c, uint32_t C) {
@@ -1476,11 +1531,20 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     memcpy(gth.t, tc, sizeof(uint32_t) * K);
     memcpy(gth.t + K, tm, sizeof(uint32_t) * K);
     gth.kpack = kpack;
+    // stage-2 screen (k_node_summary): per-scenario label union / conflict intersection of the
+    // schedulable nodes; FP_OPT_SCREEN = 0 sends every container through the pipeline
+    uint32_t *summ = nullptr;
+    if (N && fp_opt(c, FP_OPT_SCREEN, 1)) {
+        summ = (uint32_t *)fp_ws_take(c, (size_t)S * 16);
+        if (!summ) return FP_ENOMEM;
+        k_node_summary<<<S, 256, 0, st>>>(N, b->labels, b->conflict_used, b->schedulable, summ);
+        FP_HIP(hipGetLastError());
+    }
     if (ready) {  // k_scen_sort wrote order, cpu, mem and the position words
         size_t g = (SC + 1023) / 1024;
         if (g >= 64) g = (g + 7) & ~(size_t)7;
-        k_gather_payload<<<(unsigned)g, 256, 0, st>>>(S, C, order, b->req_labels, b->conflict, b->level, s_req,
-                                                      s_conf, s_idx);
+        k_gather_payload<<<(unsigned)g, 256, 0, st>>>(S, C, order, b->req_labels, b->conflict, b->level, summ,
+                                                      s_req, s_conf, s_idx);
         FP_HIP(hipGetLastError());
     } else {
         size_t g = (SC + 1023) / 1024;  // one tile of 1024 elements per block
@@ -1488,11 +1552,11 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         if (key_bytes == 4)
             k_gather_sorted<uint32_t><<<(unsigned)g, 256, 0, st>>>(
                 gth, S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
-                b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
+                b->conflict, b->level, summ, s_cpu, s_mem, s_req, s_conf, s_idx);
         else
             k_gather_sorted<uint64_t><<<(unsigned)g, 256, 0, st>>>(
                 gth, S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
-                b->conflict, b->level, s_cpu, s_mem, s_req, s_conf, s_idx);
+                b->conflict, b->level, summ, s_cpu, s_mem, s_req, s_conf, s_idx);
         FP_HIP(hipGetLastError());
     }
     PipeArgs a;

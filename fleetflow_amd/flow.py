@@ -215,6 +215,9 @@ class Plan:
     level_order: list[str]        # sort by (level, position)
     assignment: dict[str, str]    # service -> server slug (unplaced absent)
     rejected: dict[str, str]      # service -> "NOFIT" | "CYCLE"
+    # stage 2 on the stage's pristine server table: service -> (feasible servers, first feasible
+    # slug or None); count 0 is an exact NOFIT before placement (SPEC.md 2.3 monotonicity)
+    candidates: dict[str, tuple[int, str | None]] = field(default_factory=dict)
 
 
 def _server_nodes(flow: Flow, servers: list[str]):
@@ -233,7 +236,7 @@ def plan_stage(flow: Flow, stage_name: str, planner: Planner | None = None,
     order = order_by_dependencies(services, flow, p)
     levels, level_order = levelize_stage(services, flow, p)
     nodes = servers if servers is not None else _server_nodes(flow, stage.servers)
-    assignment, rejected = {}, {}
+    assignment, rejected, candidates = {}, {}, {}
     if services and nodes:
         names, pos2v, *_ = stage_graph(services, flow)
         lvl_v = {names[v]: levels[i] for i, v in enumerate(pos2v)}
@@ -263,13 +266,17 @@ def plan_stage(flow: Flow, stage_name: str, planner: Planner | None = None,
         cu = [0] * len(nodes)
         sch = [1 if nd.schedulable else 0 for nd in nodes]
         lv = [lvl_v[n] for n in names]
+        # stage 2 (fp_feasibility): feasible-server count and first feasible server per service
+        first, count, _ = p.feasibility((cpu, mem, req, conf), (cf, mf, lab, cu, sch), bitmap=False)
+        candidates = {n: (int(count[v]), nodes[int(first[v])].slug if int(first[v]) != NONE else None)
+                      for v, n in enumerate(names)}
         assign, reason, _ = p.place((cpu, mem, req, conf), (cf, mf, lab, cu, sch), level=lv)
         for v, n in enumerate(names):
             if assign[v] != NONE:
                 assignment[n] = nodes[assign[v]].slug
             else:
                 rejected[n] = "CYCLE" if reason[v] == 2 else "NOFIT"
-    return Plan(stage_name, order, dict(zip(services, levels)), level_order, assignment, rejected)
+    return Plan(stage_name, order, dict(zip(services, levels)), level_order, assignment, rejected, candidates)
 
 
 def resolve_target_server(flow: Flow, stage_name: str, planner: Planner | None = None) -> str | None:

@@ -8,7 +8,8 @@
 ``fleet up --dry-run`` (crates/fleetflow/src/commands/up.rs:57-136) and
 ``fleet deploy --dry-run`` (crates/fleetflow/src/commands/deploy.rs:14-100)
 line for line, without ANSI colour. When a ``Plan`` is given, each service
-block gains two lines, its start level and its planned server. Without one the
+block gains its start level, its candidate servers (stage 2: the feasible-server count
+and the first feasible server on the pristine table) and its planned server. Without one the
 text is the reference's. The environment line lists variables in definition
 order (the reference iterates a HashMap, so its order is arbitrary; compare it
 as a set).
@@ -30,13 +31,15 @@ def plan_to_json(plan: Plan, indent: int | None = None) -> str:
         "level_order": plan.level_order,
         "assign": plan.assignment,
         "rejected": plan.rejected,
+        "candidates": {k: {"count": c, "first": f} for k, (c, f) in plan.candidates.items()},
     }, ensure_ascii=False, indent=indent)
 
 
 def plan_from_json(text: str) -> Plan:
     d = json.loads(text)
     return Plan(d["stage"], d["order"], {k: (U32_MAX if v is None else v) for k, v in d["levels"].items()},
-                d["level_order"], d["assign"], d["rejected"])
+                d["level_order"], d["assign"], d["rejected"],
+                {k: (v["count"], v["first"]) for k, v in d.get("candidates", {}).items()})
 
 
 def get_network_name(project: str, stage: str) -> str:
@@ -67,6 +70,9 @@ def _service_block(flow: Flow, stage: str, name: str, container_suffix: str, pla
     if plan is not None:
         lv = plan.levels.get(name)
         lines.append(f"    起動レベル: {'CYCLE' if lv == U32_MAX else lv}")
+        if name in plan.candidates:  # stage 2: how many servers could take it on the pristine table
+            cnt, first = plan.candidates[name]
+            lines.append(f"    配置候補: {cnt} 台" + (f" (最初: {first})" if first else ""))
         if name in plan.assignment:
             lines.append(f"    配置先: {plan.assignment[name]}")
         elif name in plan.rejected:

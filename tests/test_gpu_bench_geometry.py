@@ -153,3 +153,42 @@ def test_systolic_batch_zero_and_cycles(thr, planner, O, opts):
         assert int(cost[s]) == O.cost(ea, N, base + s)
         for i in (0, 1, 3):
             assert np.array_equal(after[i][s * N:(s + 1) * N], eafter[i])
+
+
+# ---- stage-2 early-NOFIT screen (fp_pipe.hip k_node_summary) ------------------------------------
+@pytest.mark.parametrize("S,C,N", [(1, 20_000, 3_000), (6, 4_000, 2_000), (64, 2_000, 640)])
+def test_screen_vs_unscreened_and_oracle(S, C, N, planner, O, opts):
+    """Containers whose labels lie outside every schedulable node's labels, or whose conflict bits
+    every schedulable node has used, are rejected NOFIT before the pipeline.  The plans with and
+    without the screen, and the oracle's, must be identical; the inputs make both rules fire (one
+    scenario with every node's port 3 taken, one with no node labelled 5, cordoned nodes)."""
+    base = 11
+    rng = np.random.default_rng(S * C)
+    conts, nodes = [], []
+    for s in range(S):
+        c, n = O.gen_scenario(SEED4 + 41, base + s, C, N, 7)
+        c = [np.array(a, np.uint32) for a in c]
+        n = [np.array(a) for a in n]
+        n[4] = n[4].astype(np.uint8)
+        n[4][rng.random(N) < 0.05] = 0
+        if s % 3 == 0:
+            n[3][:] |= 1 << 3                       # port 3 used on every node
+            c[3][rng.random(C) < 0.05] |= 1 << 3
+        if s % 3 == 1:
+            n[2][:] &= ~np.uint32(1 << 5)           # nobody carries label bit 5
+            c[2][rng.random(C) < 0.05] |= 1 << 5
+        conts.append(c)
+        nodes.append(n)
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    args = ([cat(conts, i) for i in range(4)], [cat(nodes, i) for i in range(5)])
+    a1, r1, c1, n1 = planner.place_batch(S, C, N, *args, scen_base=base)
+    opts(screen=0)
+    a0, r0, c0, n0 = planner.place_batch(S, C, N, *args, scen_base=base)
+    assert np.array_equal(a1, a0) and np.array_equal(r1, r0) and np.array_equal(c1, c0)
+    for s in range(S):
+        ea, er, eafter, _ = O.place(conts[s], nodes[s])
+        assert np.array_equal(a1[s * C:(s + 1) * C], ea), s
+        assert np.array_equal(r1[s * C:(s + 1) * C], er), s
+        assert int(c1[s]) == O.cost(ea, N, base + s)
+        for i in (0, 1, 3):
+            assert np.array_equal(n1[i][s * N:(s + 1) * N], eafter[i])

@@ -70,3 +70,56 @@ def test_host_call_writes_nothing_on_error(planner):
     with pytest.raises(FleetplaceError):
         planner.levelize([0, 2, 1], [1, 0], [0, 1])  # row_ptr not monotone
     planner.sync()
+
+
+def test_pending_async_error_survives_unrelated_host_call(planner, opts):
+    """an asynchronous call's kernel error is neither reported by, nor cleared by, a
+    later unrelated host-pointer call (those have their own error word); fp_ctx_sync still
+    reports it once."""
+    import torch
+    from fleetflow_amd import DevBatch
+    from fleetflow_amd._lib import FP_EDEVICE, FleetplaceError
+    db = DevBatch.allocate(4, 50_000, 5_000, "cuda:0")
+    planner.dev_gen_batch(0x5EED0004, db, 7)
+    opts(spin_ticks=1)
+    planner.dev_place_batch(db)                              # fails asynchronously (guard)
+    planner.set_option("spin_ticks")
+    level, order, ncyc = planner.levelize([0, 1, 1], [1], [0, 1])   # unrelated host call: fine
+    assert level.tolist() == [0, 1] and ncyc == 0
+    with pytest.raises(FleetplaceError) as e:
+        planner.sync()
+    assert e.value.code == FP_EDEVICE
+    planner.sync()
+    del db
+    torch.cuda.empty_cache()
+
+
+def test_forced_bounded_links_without_residency_fail_promptly(planner, opts):
+    """bounded links on a batch whose consumers cannot be resident (forced: lag = S
+    runs segment b only after phase b - 1 drained, so a producer with a full 8-slot ring waits on
+    a consumer that has not started) must end in FP_EDEVICE from the deadlock guard, promptly,
+    and leave the context usable."""
+    import time
+    import torch
+    from fleetflow_amd import DevBatch
+    from fleetflow_amd._lib import FP_EDEVICE, FleetplaceError
+    S, C, N = 16, 20_000, 5_000
+    db = DevBatch.allocate(S, C, N, "cuda:0")
+    planner.dev_gen_batch(0x5EED0004, db, 7)
+    snap = db.node_snapshot()
+    opts(pipe_lag=S, link_bounded=1, link_slots=8, spin_ticks=20_000_000)  # 0.2 s guard
+    g = planner.geometry(S, C, N)
+    assert g["bounded"] == 1 and g["lag"] == S and g["link_slots"] == 8, g
+    t0 = time.perf_counter()
+    planner.dev_place_batch(db)
+    with pytest.raises(FleetplaceError) as e:
+        planner.sync()
+    assert e.value.code == FP_EDEVICE
+    assert time.perf_counter() - t0 < 30
+    planner.reset_options()
+    db.restore_nodes(snap)
+    planner.dev_place_batch(db)
+    planner.sync()
+    assert int((db.reason == 0).sum().item()) > 0
+    del db
+    torch.cuda.empty_cache()

@@ -198,6 +198,15 @@ def test_plan_stage_with_registry_nodes(planner, O):
             assert plan.assignment[s] == nodes[ea[i]].slug
         else:
             assert plan.rejected[s] == "NOFIT"
+    # the dry-run's stage-2 candidates (first feasible server and count on the pristine table)
+    ef, ec, _ = O.feasibility(cont, nd, want_bitmap=False)
+    for i, s in enumerate(svcs):
+        assert plan.candidates[s] == (int(ec[i]), nodes[ef[i]].slug if ef[i] != NONE else None), s
+        if ec[i] == 0:  # count 0 on the pristine table: rejected NOFIT by the placement too
+            assert plan.rejected[s] == "NOFIT"
+    from fleetflow_amd.plan_output import format_up_dry_run, plan_from_json, plan_to_json
+    assert plan_from_json(plan_to_json(plan)) == plan
+    assert format_up_dry_run(flow, "live", plan).count("    配置候補: ") == len(svcs)
 
 
 # ---- A6 FFD ------------------------------------------------------------------------------
