@@ -95,21 +95,25 @@ def test_pending_async_error_survives_unrelated_host_call(planner, opts):
 
 
 def test_forced_bounded_links_without_residency_fail_promptly(planner, opts):
-    """bounded links on a batch whose consumers cannot be resident (forced: lag = S
-    runs segment b only after phase b - 1 drained, so a producer with a full 8-slot ring waits on
-    a consumer that has not started) must end in FP_EDEVICE from the deadlock guard, promptly,
-    and leave the context usable."""
+    """bounded links on a batch whose consumers cannot be resident must end in
+    FP_EDEVICE from the deadlock guard, promptly, and leave the context usable.  Forced: lag = S
+    hands out every scenario's segment-0 ticket before any segment-1 ticket, and the batch holds
+    more scenarios than the device has segment slots, so the resident segment-0 producers fill
+    their 8-slot rings and wait on segment-1 consumers that can never be dispatched.  (With
+    every segment resident the same forced geometry completes: a consumer is always running.)"""
     import time
     import torch
     from fleetflow_amd import DevBatch
     from fleetflow_amd._lib import FP_EDEVICE, FleetplaceError
-    S, C, N = 16, 20_000, 5_000
+    C, N = 12_000, 5_000  # 7 segments of 12 groups; segment 0 (768 nodes) forwards ~4k per scenario
+    S = planner.geometry(1024, C, N)["resident"] + 256
     db = DevBatch.allocate(S, C, N, "cuda:0")
     planner.dev_gen_batch(0x5EED0004, db, 7)
     snap = db.node_snapshot()
     opts(pipe_lag=S, link_bounded=1, link_slots=8, spin_ticks=20_000_000)  # 0.2 s guard
     g = planner.geometry(S, C, N)
     assert g["bounded"] == 1 and g["lag"] == S and g["link_slots"] == 8, g
+    assert S > g["resident"] and g["segments"] > 1, g
     t0 = time.perf_counter()
     planner.dev_place_batch(db)
     with pytest.raises(FleetplaceError) as e:

@@ -23,7 +23,7 @@ def main():
     p = Planner(0)
     _opts.apply_env(p)
     db = DevBatch.allocate(S, C, N, "cuda:0")
-    p.dev_gen_batch(0x5EED0004, db, 7)
+    p.dev_gen_batch(int(os.environ.get("SEED", "0x5EED0004"), 0), db, 7)
     p.sync()  # the generator runs on the planner stream; torch copies on its own
     pristine = db.node_snapshot()
     torch.cuda.synchronize()
