@@ -1216,6 +1216,81 @@ __global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restr
     }
 }
 
+// The same payload as k_gather_payload with every HBM access coalesced: one workgroup per
+// scenario.  Each thread owns the sorted positions t + 1024 j; per half of them (25 per thread:
+// registers) it keeps their container indices, then streams the scenario's (req, conf) pairs
+// through LDS in chunks of PL_CHUNK and picks its positions' values out of the chunk that holds
+// them (level the same way first, for the CYCLE bits).  k_gather_payload's two random 4-B reads
+// per container ran at the L2 request rate (2.2 ms for 4096 x 50k).  C <= PL_MAX_C.
+constexpr uint32_t PL_THREADS = 1024, PL_H = 25, PL_MAX_C = PL_THREADS * PL_H * 2;
+constexpr uint32_t PL_CHUNK = 18 * 1024;  // (req, conf) pairs: 144 KB of LDS
+__global__ __launch_bounds__(1024) void k_payload_lds(uint32_t C, const uint32_t *__restrict__ order,
+                                                      const uint32_t *__restrict__ req,
+                                                      const uint32_t *__restrict__ conf,
+                                                      const uint32_t *__restrict__ level,
+                                                      const uint32_t *__restrict__ summ,
+                                                      uint32_t *__restrict__ s_req, uint32_t *__restrict__ s_conf,
+                                                      uint32_t *__restrict__ s_idx) {
+    extern __shared__ uint2 pl_lds2[];
+    uint32_t *pl_lds = reinterpret_cast<uint32_t *>(pl_lds2);
+    const uint32_t t = threadIdx.x;
+    const size_t cb = (size_t)blockIdx.x * C;
+    const uint32_t sm0 = summ ? summ[(size_t)blockIdx.x * 4] : 0xFFFFFFFFu;
+    const uint32_t sm1 = summ ? summ[(size_t)blockIdx.x * 4 + 1] : 0u;
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t pbase = h * PL_THREADS * PL_H + t;
+        if (h * PL_THREADS * PL_H >= C) break;  // uniform: every thread meets the same barriers
+        uint32_t o[PL_H];
+#pragma unroll
+        for (uint32_t j = 0; j < PL_H; ++j) {
+            const uint32_t p = pbase + PL_THREADS * j;
+            o[j] = p < C ? __builtin_nontemporal_load(&order[cb + p]) : 0xFFFFFFFFu;
+        }
+        uint32_t vr[PL_H], vf[PL_H];
+        uint32_t cy = 0;
+        if (level) {
+            for (uint32_t a0 = 0; a0 < C; a0 += 2 * PL_CHUNK) {
+                const uint32_t n = C - a0 < 2 * PL_CHUNK ? C - a0 : 2 * PL_CHUNK;
+                __syncthreads();
+#pragma unroll 4
+                for (uint32_t i = t; i < n; i += PL_THREADS) pl_lds[i] = __builtin_nontemporal_load(&level[cb + a0 + i]);
+                __syncthreads();
+#pragma unroll
+                for (uint32_t j = 0; j < PL_H; ++j) {
+                    const uint32_t d = o[j] - a0;
+                    if (d < n) cy |= (uint32_t)(pl_lds[d] == FP_NONE) << j;
+                }
+            }
+        }
+        for (uint32_t a0 = 0; a0 < C; a0 += PL_CHUNK) {
+            const uint32_t n = C - a0 < PL_CHUNK ? C - a0 : PL_CHUNK;
+            __syncthreads();
+#pragma unroll 4
+            for (uint32_t i = t; i < n; i += PL_THREADS)
+                pl_lds2[i] = make_uint2(__builtin_nontemporal_load(&req[cb + a0 + i]), __builtin_nontemporal_load(&conf[cb + a0 + i]));
+            __syncthreads();
+#pragma unroll
+            for (uint32_t j = 0; j < PL_H; ++j) {
+                const uint32_t d = o[j] - a0;
+                if (d < n) { const uint2 x = pl_lds2[d]; vr[j] = x.x; vf[j] = x.y; }
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < PL_H; ++j) {
+            const uint32_t p = pbase + PL_THREADS * j;
+            if (p < C) {
+                uint32_t r = vr[j];
+                const bool c = (cy >> j) & 1u, x = ((r & ~sm0) | (vf[j] & sm1)) != 0u;
+                if (c) r = FP_REASON_CYCLE;
+                else if (summ && x) r = FP_REASON_NOFIT;
+                __builtin_nontemporal_store(r, &s_req[cb + p]);
+                __builtin_nontemporal_store(vf[j], &s_conf[cb + p]);
+                if (c || (summ && x)) s_idx[cb + p] |= CYC;
+            }
+        }
+    }
+}
+
 // assign/reason from FFD (sorted) order back to container order, per scenario and per
 // range of container indices held in LDS: every read and write is coalesced.  The
 // pipeline's stores hit the sorted arrays at positions that advance together, so its
@@ -1540,7 +1615,15 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         k_node_summary<<<S, 256, 0, st>>>(N, b->labels, b->conflict_used, b->schedulable, summ);
         FP_HIP(hipGetLastError());
     }
-    if (ready) {  // k_scen_sort wrote order, cpu, mem and the position words
+    if (ready && C && C <= PL_MAX_C && fp_opt(c, FP_OPT_PAYLOAD_LDS, 1) != 0) {
+        // k_scen_sort wrote order, cpu, mem and the position words; req / conf / CYCLE bits
+        // through LDS, one workgroup per scenario
+        const size_t pl = (size_t)PL_CHUNK * 8;
+        FP_HIP(hipFuncSetAttribute((const void *)k_payload_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl));
+        k_payload_lds<<<S, PL_THREADS, pl, st>>>(C, order, b->req_labels, b->conflict, b->level, summ, s_req, s_conf,
+                                                 s_idx);
+        FP_HIP(hipGetLastError());
+    } else if (ready) {  // the same with random gathers
         size_t g = (SC + 1023) / 1024;
         if (g >= 64) g = (g + 7) & ~(size_t)7;
         k_gather_payload<<<(unsigned)g, 256, 0, st>>>(S, C, order, b->req_labels, b->conflict, b->level, summ,

@@ -156,7 +156,8 @@ enum fp_option {
     FP_OPT_LEVELIZE_SYNC = 12,/* 1 = level-synchronous Kahn instead of the async levelizer */
     FP_OPT_SYSTOLIC_EXTRA = 13, /* systolic steps past the queue length before the serial finish */
     FP_OPT_SCREEN = 14,       /* 0 = no stage-2 early-NOFIT screen: every container enters    */
-    FP_OPT_COUNT = 15
+    FP_OPT_PAYLOAD_LDS = 15,  /* 0 = random-gather payload instead of the LDS-chunked one      */
+    FP_OPT_COUNT = 16
 };
 int fp_ctx_set_option(fp_ctx *ctx, int option, int64_t value);
 int fp_ctx_get_option(fp_ctx *ctx, int option, int64_t *value);

@@ -36,6 +36,7 @@ pub const FP_OPT_SYSTOLIC: c_int = 11;
 pub const FP_OPT_LEVELIZE_SYNC: c_int = 12;
 pub const FP_OPT_SYSTOLIC_EXTRA: c_int = 13;
 pub const FP_OPT_SCREEN: c_int = 14;
+pub const FP_OPT_PAYLOAD_LDS: c_int = 15;
 pub const FP_GEOM_GROUPS: usize = 0;
 pub const FP_GEOM_STAGES: usize = 1;
 pub const FP_GEOM_SEGMENTS: usize = 2;

@@ -17,9 +17,11 @@ SEED = 0x5EED5050
 SS_MAX_C = 50_680
 
 
-@pytest.fixture(params=["scen_sort", "radix"])
+@pytest.fixture(params=["scen_sort", "scen_sort_gather", "radix"])
 def sort_path(request, opts):
-    opts(scen_sort=0 if request.param == "radix" else -1)
+    """The LDS sort with the LDS-chunked payload (k_payload_lds, default), the LDS sort with the
+    random-gather payload (k_gather_payload), and the radix-key path."""
+    opts(scen_sort=0 if request.param == "radix" else -1, payload_lds=0 if request.param == "scen_sort_gather" else -1)
     return request.param
 
 
@@ -101,6 +103,17 @@ def test_scen_sort_cycles(sort_path, planner, O):
     S, C, N = 3, 5_000, 400
     conts, nodes = zip(*[O.gen_scenario(SEED + 2, s, C, N, 7) for s in range(S)])
     level = [np.where(rng.random(C) < 0.05, 0xFFFFFFFF, rng.integers(0, 9, C)).astype(np.uint32) for _ in range(S)]
+    _batch_check(planner, O, list(conts), list(nodes), level=level)
+
+
+@pytest.mark.parametrize("C", [25_600, 25_601, 40_000])
+def test_scen_sort_cycles_chunks(C, sort_path, planner, O):
+    """Positions across both register halves of k_payload_lds (25,600 per half) and level /
+    (req, conf) arrays spanning several LDS chunks (36,864 / 18,432 containers)."""
+    rng = np.random.default_rng(C)
+    S, N = 2, 3_000
+    conts, nodes = zip(*[O.gen_scenario(SEED + 3, s, C, N, 7) for s in range(S)])
+    level = [np.where(rng.random(C) < 0.03, 0xFFFFFFFF, rng.integers(0, 5, C)).astype(np.uint32) for _ in range(S)]
     _batch_check(planner, O, list(conts), list(nodes), level=level)
 
 
