@@ -1551,6 +1551,7 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     if (g->sys > 64) g->sys = 64;
     g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
     if (g->sys_extra > 128) g->sys_extra = 128;
+    if (fp_opt(c, FP_OPT_SYSTOLIC_VALU, 0) != 0) g->sys_extra |= 0x8000u;  // fp_pipe_sysv.h step loop
     return true;
 }
 

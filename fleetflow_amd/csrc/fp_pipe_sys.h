@@ -215,6 +215,11 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     return out;
 }
 
+}  // namespace fpp
+
+#include "fp_pipe_sysv.h"
+
+namespace fpp {
 
 // Drop-in for fpp_group_x (same arguments): the systolic loop, the serial finish of what it
 // left open, and the same per-group vector epilogue (placed bits of the hits, next candidate
@@ -228,8 +233,11 @@ __device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint
     const uint32_t gbg = gb64 + g * 64u;
     // `extra`: steps the systolic phase runs past the queue length before the serial loop
     // takes the containers still open (PipeArgs::sys_extra)
-    const SysOut so = fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm,
-                                    (uint32_t)__builtin_popcountll(q) + extra);
+    // extra bit 15: the VALU-only step loop (fp_pipe_sysv.h, FP_OPT_SYSTOLIC_VALU)
+    const uint32_t cap = (uint32_t)__builtin_popcountll(q) + (extra & 0x7FFFu);
+    const SysOut so = (extra & 0x8000u)
+                          ? fpp_sysv_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap)
+                          : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap);
     uint64_t left = fpp_uniform64(so.left);
     touched = fpp_uniform64(touched);
     if (left) fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);

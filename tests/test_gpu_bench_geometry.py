@@ -104,16 +104,18 @@ def test_geometry_query_defaults(planner):
 
 
 # ---- systolic group fill (fp_pipe_sys.h) ------------------------------------------------------
+@pytest.mark.parametrize("valu", [0, 1])
 @pytest.mark.parametrize("thr", [1, 24])
 @pytest.mark.parametrize("C,N,flags,w,seg", [(20_000, 6_000, 7, 4, 4), (60_000, 12_000, 7, 4, 4),
                                              (4_000, 641, 7, 1, 12), (5_000, 5_121, 3, 1, 32),
-                                             (30_000, 2_000, 7, 4, 40), (64, 64, 7, 4, 4)])
-def test_systolic_fill_vs_oracle(C, N, flags, w, seg, thr, planner, O, opts):
+                                             (30_000, 2_000, 7, 4, 40), (64, 64, 7, 4, 4),
+                                             (40_000, 3_000, 7, 2, 2), (9_000, 700, 5, 1, 1)])
+def test_systolic_fill_vs_oracle(C, N, flags, w, seg, thr, valu, planner, O, opts):
     """Group queues of >= thr containers take the systolic loop (thr 1: every queue), the rest
     the serial one; the plan, reasons and final node state must be the oracle's.  The systolic
     loop is compiled for stages of at most 4 groups (FP_SYS_MAX_G): wider stages report 0 and
     run the serial loop on the same inputs."""
-    opts(systolic=thr, pipe_w=w, pipe_seg=seg)
+    opts(systolic=thr, pipe_w=w, pipe_seg=seg, systolic_valu=valu)
     g = planner.geometry(1, C, N)
     assert g["systolic"] == (thr if g["groups"] <= 4 else 0), g
     cont, nodes = O.gen_scenario(SEED4 + 23 * C + N, 2, C, N, flags)
@@ -125,11 +127,12 @@ def test_systolic_fill_vs_oracle(C, N, flags, w, seg, thr, planner, O, opts):
         assert np.array_equal(after[i], eafter[i])
 
 
+@pytest.mark.parametrize("valu", [0, 1])
 @pytest.mark.parametrize("thr", [1, 16])
-def test_systolic_batch_zero_and_cycles(thr, planner, O, opts):
+def test_systolic_batch_zero_and_cycles(thr, valu, planner, O, opts):
     """Systolic fill in a many-scenario batch with all-zero containers, cycles and cordoned
     nodes (the zero containers bypass the group loops; CYCLE members never enter)."""
-    opts(systolic=thr)
+    opts(systolic=thr, systolic_valu=valu)
     S, C, N, base = 6, 5_000, 3_000, 77
     rng = np.random.default_rng(thr)
     conts, nodes, levels = [], [], []

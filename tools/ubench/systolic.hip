@@ -14,6 +14,7 @@
 
 #include "fp_pipe_asm.h"
 #include "fp_pipe_sys.h"
+#include "fp_pipe_sysv.h"
 
 using namespace fpp;
 
@@ -80,8 +81,9 @@ __global__ void k_sys(uint64_t *out, uint32_t *res, int pattern, uint32_t reps, 
             fpp_group_x<0, 1>(q, placed, touched, asg, nxt, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 1u, 0u, 0u, nchk,
                               nhit, qc, qm);
         } else {
-            SysOut so = fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm,
-                                      V == 1 ? 1000u : (uint32_t)__builtin_popcountll(q) + extra);
+            const uint32_t cap = (V == 1 || V == 3) ? 1000u : (uint32_t)__builtin_popcountll(q) + extra;
+            SysOut so = V >= 3 ? fpp_sysv_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm, cap)
+                               : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm, cap);
             uint64_t left = __builtin_amdgcn_readfirstlane((uint32_t)so.left) |
                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(so.left >> 32)) << 32);
             if (left) fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, nchk);
@@ -108,19 +110,22 @@ int main() {
     hipMalloc(&d, 64 * 8);
     hipMalloc(&dr, 5 * 64 * 4);
     const uint32_t reps = 64;
-    const char *names[] = {"serial exec-masked (fpp_group_x)", "systolic, full", "systolic, Q+extra + serial"};
+    const char *names[] = {"serial exec-masked (fpp_group_x)", "systolic, full", "systolic, Q+extra + serial",
+                           "VALU systolic, full", "VALU systolic, Q+extra + serial"};
     for (int pattern : {0, 1, 2, 3, 4}) {
         uint32_t ref[320], got[320];
-        for (int v = 0; v <= 2; ++v) {
+        for (int v = 0; v <= 4; ++v) {
             for (uint32_t extra : {0u, 8u, 24u}) {
-                if (v < 2 && extra) continue;
+                if ((v < 2 || v == 3) && extra) continue;
                 for (int nw : {1, 4}) {
                     uint64_t h[64] = {0};
                     for (int it = 0; it < 2; ++it) {
                         hipMemset(d, 0, 64 * 8);
                         if (v == 0) k_sys<0><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         else if (v == 1) k_sys<1><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
-                        else k_sys<2><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else if (v == 2) k_sys<2><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else if (v == 3) k_sys<3><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else k_sys<4><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
                         hipMemcpy(h, d, 64 * 8, hipMemcpyDeviceToHost);
                     }
