@@ -88,6 +88,7 @@ struct PipeArgs {
     uint32_t bounded; // 1: links are rings with back-pressure (every segment co-resident, lag 0)
     uint32_t flush;   // idle flushes of partial output slots: bit 0 LDS rings, bit 1 global links (bounded)
     uint32_t kpack;   // 1: s_idx carries the bucket indices (bits 21-25 cpu, 26-30 mem; C <= 2^21)
+    uint32_t publish; // full slots per head publish on a global link (1 when bounded: see the kernel)
     uint32_t sys;     // systolic group fill: queues of >= (sys & 0xFFFF) containers, (sys >> 16) extra
                       // steps before the serial finish (0: serial loop only)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
@@ -474,6 +475,11 @@ k_ffd_pipe(const PipeArgs a) {
     uint32_t *idata = D + (size_t)(w - 1) * R * NF * 64;
     uint32_t *abort_flag = &CNT[2];
     uint32_t ohead = 0, ofill = 0, itail = 0, k0 = 0;
+    uint32_t ihead_seen = 0;  // last head read from the upstream link
+    // full slots written but not yet published (global link): the head store and the wait for
+    // the slot stores before it (s_waitcnt vmcnt(0)) are paid once per a.publish slots; the end
+    // of the stream publishes the rest
+    uint32_t opend = 0;
     uint32_t n_used = 0, n_rej = 0;
     uint32_t st_spin_in = 0, st_spin_out = 0, st_visits = 0, st_checks = 0, st_hits = 0, st_batches = 0;
     // diagnostics (C++ loop, stats build): why candidate checks miss -- [0] cpu and mem fit some
@@ -496,9 +502,10 @@ k_ffd_pipe(const PipeArgs a) {
             // poll the upstream segment's head (sc1), bounded; then sc1 payload loads
             uint32_t n_sp = 0;
             uint64_t t0 = 0;
-            bool got = false;
-            while (true) {
-                if (g_ld(gin_head) > itail) { got = true; break; }
+            bool got = itail < ihead_seen;  // a head seen earlier already covers this slot: no poll
+            while (!got) {
+                ihead_seen = __builtin_amdgcn_readfirstlane(g_ld(gin_head));
+                if (ihead_seen > itail) { got = true; break; }
                 if (g_ld(a.gabort) || lds_acq(abort_flag)) break;
                 if ((++n_sp & 255u) == 0) {
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -875,9 +882,12 @@ k_ffd_pipe(const PipeArgs a) {
                 }
                 if (ofill + f >= 64) {
                     if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, 64u);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     ohead++;
-                    if (lane == 0) g_st(gout_head, ohead);
+                    if (++opend >= a.publish) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) g_st(gout_head, ohead);
+                        opend = 0;
+                    }
                     ofill = ofill + f - 64;
                 } else {
                     ofill += f;
@@ -890,6 +900,7 @@ k_ffd_pipe(const PipeArgs a) {
                 ohead++;
                 if (lane == 0) g_st(gout_head, ohead);
                 ofill = 0;
+                opend = 0;
             }
             continue;
         }
@@ -1661,6 +1672,14 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.assign = asg_s; a.reason = rsn_s; a.cost = b->cost; a.err = c->d_err;
     a.spin_ticks = (uint64_t)fp_opt(c, FP_OPT_SPIN_TICKS, (int64_t)SPIN_TICKS);
     a.sys = geo.sys ? (geo.sys | (geo.sys_extra << 16)) : 0u;
+    // Head publishes on a link that holds every container (lag = S: the consumer runs a phase
+    // later) are batched: FP_OPT_LINK_PUBLISH full slots per head store and vmcnt(0) drain.  A
+    // bounded ring publishes every slot: its producer may wait on the consumer's tail, which
+    // moves only on published slots.
+    {
+        const int64_t pv = fp_opt(c, FP_OPT_LINK_PUBLISH, 32);
+        a.publish = geo.bounded ? 1u : (uint32_t)(pv < 1 ? 1 : pv > 1024 ? 1024 : pv);
+    }
     // bucket thresholds (fp_place.hip chooses them; any ascending choice with T0 = 0 is
     // exact -- it only decides how tight the candidate masks are)
     memcpy(a.tc, tc, sizeof(a.tc));

@@ -61,15 +61,17 @@ def test_config4_exact_bench_call(planner, O):
 
 # (S, groups per segment) -> 5000 nodes = 79 groups: seg 40 -> B = 2, 28 -> 3, 20 -> 4, 16 -> 5,
 # 12 -> 7 (one-wave segments)
-@pytest.mark.parametrize("S,seg", [(5, 40), (9, 28), (13, 20), (5, 16), (9, 12), (13, 12)])
+@pytest.mark.parametrize("S,seg,publish", [(5, 40, 1), (9, 28, 3), (13, 20, 8), (5, 16, 1024), (9, 12, 1),
+                                            (13, 12, 8), (13, 12, 2)])
 @pytest.mark.parametrize("lag", ["S", 3])
-def test_forced_lag_geometries(S, seg, lag, planner, O, opts):
+def test_forced_lag_geometries(S, seg, publish, lag, planner, O, opts):
     """Segment ticket lag forced on a small batch: ticket t -> round t / B, segment t % B,
     scenario round - segment * lag.  lag = S is the bench's phased schedule; lag 3 interleaves
-    phases.  Unbounded links (a consumer may start after its producer ended)."""
+    phases.  Unbounded links (a consumer may start after its producer ended), with the head
+    published every `publish` full slots (1 .. the whole stream)."""
     C, N, base = 3_000, 5_000, 40
     lagv = S if lag == "S" else lag
-    opts(pipe_w=1, pipe_seg=seg, pipe_lag=lagv)
+    opts(pipe_w=1, pipe_seg=seg, pipe_lag=lagv, link_publish=publish)
     geo = planner.geometry(S, C, N)
     assert geo["lag"] == lagv and geo["bounded"] == 0 and geo["stages"] == 1, geo
     B = geo["segments"]
