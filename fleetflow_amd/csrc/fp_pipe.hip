@@ -494,6 +494,12 @@ k_ffd_pipe(const PipeArgs a) {
     unsigned long long sp_first = 0;
 #endif
     bool alive = true;
+#ifdef FP_PREFETCH
+    // the next batch's input, loaded while this batch is processed (FP_PREFETCH builds):
+    // segment 0 the five sorted fields, a link consumer the next slot's count and positions
+    uint32_t pf_cpu = 0, pf_mem = 0, pf_req = 0, pf_conf = 0, pf_idx = 0, pf_n = 0;
+    bool pf_have = false;
+#endif
     while (alive) {
         ck_a = STAT_CLK();
         uint32_t cpu = 0, mem = 0, req = 0, conf = 0, idx = 0;
@@ -531,8 +537,20 @@ k_ffd_pipe(const PipeArgs a) {
             // published every slot then.
             if (((a.flush & 2u) || (gbounded && (itail & 3u) == 0)) && lane == 0) g_st(gin_head + LCTL / 2, itail);
             const uint32_t *sd = gin_data + (size_t)(itail % gslots) * LSLOT;
+#ifdef FP_PREFETCH
+            const uint32_t n = pf_have ? pf_n : g_ld(sd);
+            const uint32_t pos = pf_have ? pf_idx : g_ld(sd + 64 + lane);
+            pf_have = false;
+            if (!(n & END) && itail + 1u < ihead_seen) {  // the next slot is published: load it now
+                const uint32_t *sn = gin_data + (size_t)((itail + 1u) % gslots) * LSLOT;
+                pf_n = g_ld(sn);
+                pf_idx = g_ld(sn + 64 + lane);
+                pf_have = true;
+            }
+#else
             const uint32_t n = g_ld(sd);
             const uint32_t pos = g_ld(sd + 64 + lane);  // with the count: one round trip
+#endif
             if (n & END) break;
             valid = lane < n;
             if (valid) {
@@ -548,6 +566,26 @@ k_ffd_pipe(const PipeArgs a) {
             if (k0 >= C) break;
             const uint32_t i = k0 + lane;
             valid = i < C;
+#ifdef FP_PREFETCH
+            if (pf_have) {
+                cpu = pf_cpu; mem = pf_mem; req = pf_req; conf = pf_conf; idx = pf_idx;
+            } else if (valid) {
+                cpu = a.s_cpu[cb + i];
+                mem = a.s_mem[cb + i];
+                req = a.s_req[cb + i];
+                conf = a.s_conf[cb + i];
+                idx = a.s_idx[cb + i];
+            }
+            pf_have = k0 + 64u < C;
+            if (pf_have && k0 + 64u + lane < C) {
+                const uint32_t i2 = k0 + 64u + lane;
+                pf_cpu = a.s_cpu[cb + i2];
+                pf_mem = a.s_mem[cb + i2];
+                pf_req = a.s_req[cb + i2];
+                pf_conf = a.s_conf[cb + i2];
+                pf_idx = a.s_idx[cb + i2];
+            }
+#else
             if (valid) {
                 cpu = a.s_cpu[cb + i];
                 mem = a.s_mem[cb + i];
@@ -555,6 +593,7 @@ k_ffd_pipe(const PipeArgs a) {
                 conf = a.s_conf[cb + i];
                 idx = a.s_idx[cb + i];
             }
+#endif
             const bool cyc = valid && (idx & CYC);
             if (cyc) {  // CYCLE member, or screened out by stage 2 (NOFIT): s_req holds the reason
                 const uint32_t j = idx & pmask;
