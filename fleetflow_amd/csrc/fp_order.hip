@@ -270,13 +270,6 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
     uint64_t pent[kLaneEdges + 1];
     uint64_t *pq = Q;
     while (true) {
-        if (npend) {
-            const uint32_t base = __shfl(pbase, 0);
-#pragma unroll
-            for (uint32_t k = 0; k <= kLaneEdges; ++k)
-                if (pend[k]) __hip_atomic_store(&pq[base + pofs[k]], pent[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            npend = 0;
-        }
         // one round: the poll of a claimed slot and one edge step of an item are issued
         // together, so a busy wave's polls cost no extra round trip
         uint64_t x = kQEmpty;
@@ -336,15 +329,30 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         uint32_t w[kLaneEdges], wl[kLaneEdges];
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k) ready[k] = false;
+        // the records of this round's edges are loaded first; the previous round's deferred
+        // pushes are stored after that, so waiting for their slot reservation (an atomic on a
+        // shared tail) overlaps the record load instead of preceding it -- on a chain the two
+        // were serial round trips per hop
+        const uint32_t ne = has_item ? min(e1 - e, kLaneEdges) : 0u;
+        uint4 erv[kLaneEdges];
+#pragma unroll
+        for (uint32_t k = 0; k < kLaneEdges; ++k)
+            if (k < ne) erv[k] = erec[e + k];
+        if (npend) {
+            const uint32_t base = __shfl(pbase, 0);
+#pragma unroll
+            for (uint32_t k = 0; k <= kLaneEdges; ++k)
+                if (pend[k]) __hip_atomic_store(&pq[base + pofs[k]], pent[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            npend = 0;
+        }
         if (has_item) {
-            const uint32_t ne = min(e1 - e, kLaneEdges);
             uint32_t p0[kLaneEdges], p1[kLaneEdges];
             uint64_t cur[kLaneEdges], obs[kLaneEdges];
             bool only[kLaneEdges];
 #pragma unroll
             for (uint32_t k = 0; k < kLaneEdges; ++k)
                 if (k < ne) {  // the child and its edge range (the continuation's) in one record
-                    const uint4 er = erec[e + k];
+                    const uint4 er = erv[k];
                     w[k] = er.x; p0[k] = er.y; p1[k] = er.z; only[k] = er.w != 0u;
                 }
             // first attempt guesses an untouched vertex with deps and one parent (a chain link)

@@ -248,8 +248,18 @@ using RecT = uint32_t[G];
 // are broadcast one at a time and every lane tests its own container.  It pays while the
 // corner holds few nodes (the filled-up frontier group); above FP_PF_MAX nodes the queue
 // goes to the serial loop unfiltered.
-#ifndef FP_PF_MAX
-#define FP_PF_MAX 16
+// Corner-node limit of the prefilter, by stage width (tools/gpu_ab_lib.sh, r03m_ab*.jsonl):
+// narrow (<= 4-group) stages 4 -- config 3 65.3 -> 64.1 ms (16: 65.3, 32: 70.8); wide stages
+// off -- config 4 17.54 -> 17.28 ms (4: 17.48, 32: 17.96).  FP_PF_MAX overrides both.
+#ifdef FP_PF_MAX
+#define FP_PF_MAX_NARROW FP_PF_MAX
+#define FP_PF_MAX_WIDE FP_PF_MAX
+#endif
+#ifndef FP_PF_MAX_NARROW
+#define FP_PF_MAX_NARROW 4
+#endif
+#ifndef FP_PF_MAX_WIDE
+#define FP_PF_MAX_WIDE 0
 #endif
 // systolic group fill (fp_pipe_sys.h) in stages of at most this many groups
 #ifndef FP_SYS_MAX_G
@@ -269,12 +279,13 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
                                            uint32_t &nhit, uint32_t sys) {
+    constexpr uint32_t pf_max = G <= FP_SYS_MAX_G ? FP_PF_MAX_NARROW : FP_PF_MAX_WIDE;
     (
         [&] {
             uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
-            if (FP_PF_MAX > 0 && q) {
+            if (pf_max > 0 && q) {
                 uint64_t e = __builtin_amdgcn_ballot_w64((rcf[gs] >= qc) & (rmf[gs] >= qm));
-                if (__builtin_popcountll(e) <= FP_PF_MAX) {
+                if (__builtin_popcountll(e) <= pf_max) {
                     bool ok = false;
                     while (e) {
                         const uint32_t l = (uint32_t)__builtin_ctzll(e);
@@ -494,12 +505,6 @@ k_ffd_pipe(const PipeArgs a) {
     unsigned long long sp_first = 0;
 #endif
     bool alive = true;
-#ifdef FP_PREFETCH
-    // the next batch's input, loaded while this batch is processed (FP_PREFETCH builds):
-    // segment 0 the five sorted fields, a link consumer the next slot's count and positions
-    uint32_t pf_cpu = 0, pf_mem = 0, pf_req = 0, pf_conf = 0, pf_idx = 0, pf_n = 0;
-    bool pf_have = false;
-#endif
     while (alive) {
         ck_a = STAT_CLK();
         uint32_t cpu = 0, mem = 0, req = 0, conf = 0, idx = 0;
@@ -537,20 +542,8 @@ k_ffd_pipe(const PipeArgs a) {
             // published every slot then.
             if (((a.flush & 2u) || (gbounded && (itail & 3u) == 0)) && lane == 0) g_st(gin_head + LCTL / 2, itail);
             const uint32_t *sd = gin_data + (size_t)(itail % gslots) * LSLOT;
-#ifdef FP_PREFETCH
-            const uint32_t n = pf_have ? pf_n : g_ld(sd);
-            const uint32_t pos = pf_have ? pf_idx : g_ld(sd + 64 + lane);
-            pf_have = false;
-            if (!(n & END) && itail + 1u < ihead_seen) {  // the next slot is published: load it now
-                const uint32_t *sn = gin_data + (size_t)((itail + 1u) % gslots) * LSLOT;
-                pf_n = g_ld(sn);
-                pf_idx = g_ld(sn + 64 + lane);
-                pf_have = true;
-            }
-#else
             const uint32_t n = g_ld(sd);
             const uint32_t pos = g_ld(sd + 64 + lane);  // with the count: one round trip
-#endif
             if (n & END) break;
             valid = lane < n;
             if (valid) {
@@ -566,26 +559,6 @@ k_ffd_pipe(const PipeArgs a) {
             if (k0 >= C) break;
             const uint32_t i = k0 + lane;
             valid = i < C;
-#ifdef FP_PREFETCH
-            if (pf_have) {
-                cpu = pf_cpu; mem = pf_mem; req = pf_req; conf = pf_conf; idx = pf_idx;
-            } else if (valid) {
-                cpu = a.s_cpu[cb + i];
-                mem = a.s_mem[cb + i];
-                req = a.s_req[cb + i];
-                conf = a.s_conf[cb + i];
-                idx = a.s_idx[cb + i];
-            }
-            pf_have = k0 + 64u < C;
-            if (pf_have && k0 + 64u + lane < C) {
-                const uint32_t i2 = k0 + 64u + lane;
-                pf_cpu = a.s_cpu[cb + i2];
-                pf_mem = a.s_mem[cb + i2];
-                pf_req = a.s_req[cb + i2];
-                pf_conf = a.s_conf[cb + i2];
-                pf_idx = a.s_idx[cb + i2];
-            }
-#else
             if (valid) {
                 cpu = a.s_cpu[cb + i];
                 mem = a.s_mem[cb + i];
@@ -593,7 +566,6 @@ k_ffd_pipe(const PipeArgs a) {
                 conf = a.s_conf[cb + i];
                 idx = a.s_idx[cb + i];
             }
-#endif
             const bool cyc = valid && (idx & CYC);
             if (cyc) {  // CYCLE member, or screened out by stage 2 (NOFIT): s_req holds the reason
                 const uint32_t j = idx & pmask;
@@ -1666,10 +1638,13 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         k_node_summary<<<S, 256, 0, st>>>(N, b->labels, b->conflict_used, b->schedulable, summ);
         FP_HIP(hipGetLastError());
     }
-    if (ready && C && C <= PL_MAX_C && fp_opt(c, FP_OPT_PAYLOAD_LDS, 1) != 0) {
+    const int64_t pl_mode = fp_opt(c, FP_OPT_PAYLOAD_LDS, 1);
+    if (ready && C && C <= PL_MAX_C && pl_mode != 0) {
         // k_scen_sort wrote order, cpu, mem and the position words; req / conf / CYCLE bits
         // through LDS, one workgroup per scenario
         const size_t pl = (size_t)PL_CHUNK * 8;
+        // (a one-sweep variant writing each position in the chunk pass that holds its container
+        // -- partial lines per pass -- ran 3.6 ms slower per config-4 step: r03k_payload_ab.jsonl)
         FP_HIP(hipFuncSetAttribute((const void *)k_payload_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl));
         k_payload_lds<<<S, PL_THREADS, pl, st>>>(C, order, b->req_labels, b->conflict, b->level, summ, s_req, s_conf,
                                                  s_idx);

@@ -37,10 +37,14 @@ class Planner:
         check(self._L.fp_ctx_create(ct.byref(h), device), "fp_ctx_create")
         self._ctx = h
         self.device = device
+        self._tstream = None  # torch view of the stream the dev_* calls launch on (see _dev)
 
     # -- lifetime ---------------------------------------------------------------
     def close(self):
         if getattr(self, "_ctx", None):
+            if getattr(self, "_tstream", None) is not None:
+                self._L.fp_ctx_reset_stream(self._ctx)  # off the torch stream before it can go away
+                self._tstream = None
             self._L.fp_ctx_destroy(self._ctx)
             self._ctx = None
 
@@ -59,9 +63,31 @@ class Planner:
     def set_stream(self, hip_stream_handle: int):
         """Launch on this hipStream_t handle; 0 is the HIP null (default) stream."""
         check(self._L.fp_ctx_set_stream(self._ctx, ct.c_void_p(int(hip_stream_handle))), "fp_ctx_set_stream")
+        import torch
+        self._tstream = torch.cuda.ExternalStream(int(hip_stream_handle), device=torch.device("cuda", self.device))
 
     def reset_stream(self):
         check(self._L.fp_ctx_reset_stream(self._ctx), "fp_ctx_reset_stream")
+        self._tstream = None
+
+    def _dev(self, fn, *args):
+        """Run one fp_dev_* call ordered with torch's current stream on both sides: the call
+        waits for work queued there before it (a restore_nodes copy, a tensor fill) and later
+        work there waits for the call (a snapshot, a comparison).  Stream-ordered, no host
+        sync.  The context launches on a torch-created stream unless set_stream chose one."""
+        import torch
+        cur = torch.cuda.current_stream(self.device)
+        if self._tstream is None:
+            st = torch.cuda.Stream(device=torch.device("cuda", self.device))
+            check(self._L.fp_ctx_set_stream(self._ctx, ct.c_void_p(st.cuda_stream)), "fp_ctx_set_stream")
+            self._tstream = st
+        if self._tstream.cuda_stream == cur.cuda_stream:
+            return fn(*args)
+        self._tstream.wait_stream(cur)
+        try:
+            return fn(*args)
+        finally:
+            cur.wait_stream(self._tstream)
 
     def sync(self):
         check(self._L.fp_ctx_sync(self._ctx), "fp_ctx_sync")
@@ -165,15 +191,15 @@ class Planner:
 
     # -- device-pointer API -------------------------------------------------------------
     def dev_gen_batch(self, seed, db: "DevBatch", flags=7):
-        check(self._L.fp_dev_gen_batch(self._ctx, ct.c_uint64(seed), ct.byref(db.struct()), flags),
-              "fp_dev_gen_batch")
+        self._dev(lambda: check(self._L.fp_dev_gen_batch(self._ctx, ct.c_uint64(seed), ct.byref(db.struct()), flags),
+                                "fp_dev_gen_batch"))
 
     def dev_place_batch(self, db: "DevBatch"):
-        check(self._L.fp_dev_place_batch(self._ctx, ct.byref(db.struct())), "fp_dev_place_batch")
+        self._dev(lambda: check(self._L.fp_dev_place_batch(self._ctx, ct.byref(db.struct())), "fp_dev_place_batch"))
 
     def dev_argmin_cost(self, cost_t, out_t):
-        check(self._L.fp_dev_argmin_cost(self._ctx, cost_t.data_ptr(), cost_t.numel(), out_t.data_ptr()),
-              "fp_dev_argmin_cost")
+        self._dev(lambda: check(self._L.fp_dev_argmin_cost(self._ctx, cost_t.data_ptr(), cost_t.numel(),
+                                                           out_t.data_ptr()), "fp_dev_argmin_cost"))
 
     def dev_feasibility(self, db: "DevBatch", first_t, count_t, bitmap_t=None, scenario=0):
         C, N = db.C, db.N
@@ -182,9 +208,9 @@ class Planner:
                           db.conf[o:].data_ptr())
         ns = FpNodes(N, db.cf[p:].data_ptr(), db.mf[p:].data_ptr(), db.lab[p:].data_ptr(), db.cu[p:].data_ptr(),
                      db.sched[p:].data_ptr())
-        check(self._L.fp_dev_feasibility(self._ctx, ct.byref(cs), ct.byref(ns), first_t.data_ptr(),
-                                         count_t.data_ptr(), bitmap_t.data_ptr() if bitmap_t is not None else None),
-              "fp_dev_feasibility")
+        self._dev(lambda: check(self._L.fp_dev_feasibility(
+            self._ctx, ct.byref(cs), ct.byref(ns), first_t.data_ptr(), count_t.data_ptr(),
+            bitmap_t.data_ptr() if bitmap_t is not None else None), "fp_dev_feasibility"))
 
     def place_ws_bytes(self, S: int, C: int, N: int) -> int:
         """Device workspace bytes a place batch of S x C x N takes on this context."""
@@ -194,15 +220,15 @@ class Planner:
 
     def dev_feasibility_batch(self, db: "DevBatch", first_t, count_t):
         """Stage 2 over every scenario of ``db`` ([S*C] outputs, scenario-major)."""
-        check(self._L.fp_dev_feasibility_batch(self._ctx, ct.byref(db.struct()), first_t.data_ptr(),
-                                               count_t.data_ptr()), "fp_dev_feasibility_batch")
+        self._dev(lambda: check(self._L.fp_dev_feasibility_batch(self._ctx, ct.byref(db.struct()), first_t.data_ptr(),
+                                                                 count_t.data_ptr()), "fp_dev_feasibility_batch"))
 
     def dev_levelize(self, row_ptr_t, col_t, has_deps_t, level_t, order_t, ncyc_t):
         V = has_deps_t.numel()
         g = FpGraph(V, col_t.numel(), row_ptr_t.data_ptr(), col_t.data_ptr() if col_t.numel() else None,
                     has_deps_t.data_ptr())
-        check(self._L.fp_dev_levelize(self._ctx, ct.byref(g), level_t.data_ptr(), order_t.data_ptr(),
-                                      ncyc_t.data_ptr()), "fp_dev_levelize")
+        self._dev(lambda: check(self._L.fp_dev_levelize(self._ctx, ct.byref(g), level_t.data_ptr(), order_t.data_ptr(),
+                                                        ncyc_t.data_ptr()), "fp_dev_levelize"))
 
 
 @dataclass

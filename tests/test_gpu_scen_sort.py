@@ -19,9 +19,10 @@ SS_MAX_C = 50_680
 
 @pytest.fixture(params=["scen_sort", "scen_sort_gather", "radix"])
 def sort_path(request, opts):
-    """The LDS sort with the LDS-chunked payload (k_payload_lds, default), the LDS sort with the
-    random-gather payload (k_gather_payload), and the radix-key path."""
-    opts(scen_sort=0 if request.param == "radix" else -1, payload_lds=0 if request.param == "scen_sort_gather" else -1)
+    """The LDS sort with the LDS-chunked payload (k_payload_lds, default), with the random-gather
+    payload (k_gather_payload), and the radix-key path."""
+    pl = {"scen_sort_gather": 0}.get(request.param, -1)
+    opts(scen_sort=0 if request.param == "radix" else -1, payload_lds=pl)
     return request.param
 
 

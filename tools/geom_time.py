@@ -10,6 +10,7 @@ for N in (3000, 1500):
     _opts.apply_env(p)
     db = DevBatch.allocate(S, C, N, "cuda:0")
     p.dev_gen_batch(0x5EED0004, db, 7)
+    p.sync()
     snap = db.node_snapshot()
     p.profile(True)
     ts = []

@@ -1,0 +1,17 @@
+"""Config-5 levelization timing (bench.py's levelize_leg, kernel and wall ms) on cuda:0."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from fleetflow_amd import Planner  # noqa: E402
+
+with Planner(0) as p:
+    for _ in range(2):
+        lv, _, _, _ = bench.levelize_leg(p, torch.device("cuda", 0), 10)
+        print(json.dumps({k: lv[k] for k in ("ms_per_step", "kernel_ms", "levels", "cycle_vertices")}), flush=True)

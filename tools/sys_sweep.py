@@ -41,6 +41,7 @@ def main():
             S, C, N, seed = LOADS[load]
             db = DevBatch.allocate(S, C, N, dev)
             p.dev_gen_batch(seed, db, 7)
+            p.sync()
             snap = db.node_snapshot()
             ref = None
             for v in [int(x) for x in args.values.split(",")]:
