@@ -1644,7 +1644,8 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         // through LDS, one workgroup per scenario
         const size_t pl = (size_t)PL_CHUNK * 8;
         // (a one-sweep variant writing each position in the chunk pass that holds its container
-        // -- partial lines per pass -- ran 3.6 ms slower per config-4 step: r03k_payload_ab.jsonl)
+        // -- partial lines per pass -- ran 3.6 ms slower per config-4 step, in a sweep whose inputs
+        // were not yet synchronised with the generator: r03k_payload_ab.jsonl; dropped)
         FP_HIP(hipFuncSetAttribute((const void *)k_payload_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl));
         k_payload_lds<<<S, PL_THREADS, pl, st>>>(C, order, b->req_labels, b->conflict, b->level, summ, s_req, s_conf,
                                                  s_idx);

@@ -38,12 +38,10 @@ LEGS = [("config4", int(os.environ.get("S_DIAG", 4096)), 50_000, 5_000, 0x5EED00
 
 
 def geom(p, S, C, N):
-    L = _lib.load()
-    f = L.fp_debug_pipe_geom
-    f.argtypes = [ct.c_void_p, ct.c_uint32, ct.c_uint32, ct.c_uint32, ct.POINTER(ct.c_uint32)]
-    out = (ct.c_uint32 * 8)()
-    assert f(p._ctx, S, C, N, out) == 0
-    return dict(zip(["G", "W", "B", "R", "lag", "link_slots", "bounded", "resident_segments"], list(out)))
+    g = p.geometry(S, C, N)  # fp_place_geometry (the product ABI)
+    return {"G": g["groups"], "W": g["stages"], "B": g["segments"], "R": g["ring"], "lag": g["lag"],
+            "link_slots": g["link_slots"], "bounded": g["bounded"], "resident_segments": g["resident"],
+            "systolic": g["systolic"]}
 
 
 def clock_ghz(p):
