@@ -208,12 +208,26 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // only parent is the expanding vertex is ready without an atomic (its level is the parent's
 // + 1 >= has_deps; nothing else ever touches its state word).  Round 2 paid three: col[e],
 // then row_ptr[w] beside the CAS on state[w], then the next col.
+// Round 3 adds a second record per edge, the hop after it: the child's FIRST edge (its first
+// dependent w2, w2's edge range, whether that edge is w2's only in-edge).  When the child w is
+// ready with its only parent and w2 is ready with its only parent w, a lane jumps two levels in
+// one round trip: level(w) = level(u) + 1, level(w2) = level(w) + 1, no atomic on either, and the
+// rest of w's edges go to the queue as a partial item.  A chain of depth D takes ~D/2 rounds.
 __global__ void k_edge_rec(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t E,
-                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec) {
+                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec,
+                           uint4 *__restrict__ rec2) {
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t w = col[e];
-        rec[e] = w < V ? make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u)
-                       : make_uint4(w, 0u, 0u, 0u);  // corrupt: k_indeg raised FP_ECORRUPT, no expansion runs
+        uint4 r = make_uint4(w, 0u, 0u, 0u), r2 = make_uint4(0u, 0u, 0u, 0u);
+        if (w < V) {  // else corrupt: k_indeg raised FP_ECORRUPT, no expansion runs
+            r = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
+            if (r.z > r.y) {
+                const uint32_t w2 = col[r.y];
+                if (w2 < V) r2 = make_uint4(w2, row_ptr[w2], row_ptr[w2 + 1], indeg[w2] == 1u ? 1u : 0u);
+            }
+        }
+        rec[e] = r;
+        rec2[e] = r2;
     }
 }
 
@@ -246,7 +260,7 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
 }
 
 __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
-                                                  uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
+                                                  const uint4 *__restrict__ erec2, uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
                                                   uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
                                                   uint32_t *__restrict__ err, bool pk) {
     const uint32_t lane = threadIdx.x & 63;
@@ -324,7 +338,7 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         }
         // per-lane step: up to kLaneEdges edges at once (loads and first CAS attempts all in
         // flight together), so a chain link with a few fan-out children still takes one round
-        bool ready[kLaneEdges], fin_item = false, part = false;
+        bool ready[kLaneEdges], fin_item = false, part = false, skip1 = false;
         uint64_t pent_part = 0;
         uint32_t w[kLaneEdges], wl[kLaneEdges];
 #pragma unroll
@@ -334,10 +348,11 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         // shared tail) overlaps the record load instead of preceding it -- on a chain the two
         // were serial round trips per hop
         const uint32_t ne = has_item ? min(e1 - e, kLaneEdges) : 0u;
-        uint4 erv[kLaneEdges];
+        uint4 erv[kLaneEdges], erv2 = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k)
             if (k < ne) erv[k] = erec[e + k];
+        if (pk && ne) erv2 = erec2[e];  // the hop after edge e (two-level jump, k_edge_rec)
         if (npend) {
             const uint32_t base = __shfl(pbase, 0);
 #pragma unroll
@@ -386,6 +401,19 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                         wl[k] = (uint32_t)(cur[k] >> 32);
                         if (cw == FP_NONE) {
                             cw = w[k]; cl = wl[k]; ce = p0[k]; ce1 = p1[k];
+                            // two-level jump: w ready through its only parent (this edge) and
+                            // its first dependent w2 ready through w alone -- w is final here,
+                            // the lane continues at w2, and w's other edges (if any) are queued
+                            // as a partial item skipping the first
+                            if (k == 0 && only[0] && erv2.w != 0u && pk) {
+                                level[cw] = cl;
+                                my_max = max(my_max, cl);
+                                if (ce + 1u < ce1) {
+                                    ready[0] = true;
+                                    skip1 = true;
+                                }
+                                cw = erv2.x; cl = cl + 1u; ce = erv2.y; ce1 = erv2.z;
+                            }
                         } else {
                             ready[k] = true;
                         }
@@ -461,7 +489,8 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             for (uint32_t k = 0; k <= kLaneEdges; ++k) {
                 pend[k] = k < kLaneEdges ? ready[k] : part;
                 pofs[k] = run + (uint32_t)__popcll(rm[k] & lt);
-                pent[k] = k < kLaneEdges ? ((uint64_t)(pk ? wl[k] << 8 : wl[k]) << 32) | w[k] : pent_part;
+                pent[k] = k < kLaneEdges ? ((uint64_t)(pk ? (wl[k] << 8) | (k == 0 && skip1 ? 1u : 0u) : wl[k]) << 32) | w[k]
+                                         : pent_part;
                 run += (uint32_t)__popcll(rm[k]);
             }
             npend = 1;
@@ -566,7 +595,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     // cnt[L] = frontier size of level L (one counter per possible level: <= V + 1)
     const size_t ncnt = (size_t)V + 2;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + (size_t)V * 8 * (1 + kShards) +
-                                   (size_t)E * 16 + kCtlWords * 4 + 21 * 256);
+                                   (size_t)E * 32 + kCtlWords * 4 + 22 * 256);  // erec + erec2
     if (rc) return rc;
     fp_ws_reset(c);
     uint32_t *indeg = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
@@ -600,7 +629,8 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         uint64_t *Q = (uint64_t *)fp_ws_take(c, (size_t)V * 8 * kShards);
         uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
         uint4 *erec = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
-        if (!state || !Q || !actl || (E && !erec)) return FP_ENOMEM;
+        uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
+        if (!state || !Q || !actl || (E && (!erec || !erec2))) return FP_ENOMEM;
         FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
         FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
         // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
@@ -612,10 +642,10 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         if ((rc = fp_take_err(c))) return rc;
         if (E) {
             k_edge_rec<<<blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192, 256, 0, st>>>(g->row_ptr, g->col, E, V,
-                                                                                            indeg, erec);
+                                                                                            indeg, erec, erec2);
             FP_HIP(hipGetLastError());
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
-            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, V, state, Q, actl, level, c->d_err, pk);
+            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, erec2, V, state, Q, actl, level, c->d_err, pk);
             FP_HIP(hipGetLastError());
         }
         FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &actl[26 * kCtlStride], 4, hipMemcpyDeviceToHost, st));
