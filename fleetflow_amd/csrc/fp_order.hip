@@ -186,6 +186,8 @@ constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B l
 constexpr uint64_t kQEmpty = ~0ull;
 constexpr uint32_t kCoopEdges = 16;       // edges left at which the wave expands a vertex together
 constexpr uint32_t kLaneEdges = 1;        // edges a lane relaxes per round
+constexpr uint32_t kHops = 4;             // levels a lane may jump per round along only-parent first edges
+constexpr uint32_t kPush = kLaneEdges + kHops;  // queue entries a lane may push per round
 // ctl layout (u32 index): head[s] = s*32, tail[s] = (8+s)*32, done[s] = (16+s)*32,
 // fin = 24*32, abort = 25*32, maxlvl = 26*32
 constexpr uint32_t kCtlWords = 27 * kCtlStride;
@@ -208,26 +210,37 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // only parent is the expanding vertex is ready without an atomic (its level is the parent's
 // + 1 >= has_deps; nothing else ever touches its state word).  Round 2 paid three: col[e],
 // then row_ptr[w] beside the CAS on state[w], then the next col.
-// Round 3 adds a second record per edge, the hop after it: the child's FIRST edge (its first
-// dependent w2, w2's edge range, whether that edge is w2's only in-edge).  When the child w is
-// ready with its only parent and w2 is ready with its only parent w, a lane jumps two levels in
-// one round trip: level(w) = level(u) + 1, level(w2) = level(w) + 1, no atomic on either, and the
-// rest of w's edges go to the queue as a partial item.  A chain of depth D takes ~D/2 rounds.
+// Round 3 adds kHops - 1 records per edge, the hops after it along first edges: rec2[h][e] is
+// the h-th vertex reached from the edge's child by always taking the first edge (that vertex,
+// its edge range, whether the edge into it is its only in-edge).  When the child w is ready with
+// its only parent and its first dependent w2 has w as its only parent (and so on), a lane jumps
+// several levels in one round trip: each level is the previous + 1, no atomic on any of them,
+// and the rest of each passed vertex's edges goes to the queue as a partial item.  A chain of
+// depth D takes ~D / kHops rounds.  (Two levels per round: config-5 levelize 1.51 -> 1.13 ms.)
 __global__ void k_edge_rec(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t E,
                            uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec,
                            uint4 *__restrict__ rec2) {
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t w = col[e];
-        uint4 r = make_uint4(w, 0u, 0u, 0u), r2 = make_uint4(0u, 0u, 0u, 0u);
+        uint4 r = make_uint4(w, 0u, 0u, 0u);
+        bool go = false;
         if (w < V) {  // else corrupt: k_indeg raised FP_ECORRUPT, no expansion runs
             r = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
-            if (r.z > r.y) {
-                const uint32_t w2 = col[r.y];
-                if (w2 < V) r2 = make_uint4(w2, row_ptr[w2], row_ptr[w2 + 1], indeg[w2] == 1u ? 1u : 0u);
-            }
+            go = true;
         }
         rec[e] = r;
-        rec2[e] = r2;
+        uint4 cur = r;
+#pragma unroll
+        for (uint32_t h = 0; h + 1 < kHops; ++h) {
+            uint4 n = make_uint4(0u, 0u, 0u, 0u);
+            if (go && cur.z > cur.y) {
+                const uint32_t w2 = col[cur.y];
+                if (w2 < V) n = make_uint4(w2, row_ptr[w2], row_ptr[w2 + 1], indeg[w2] == 1u ? 1u : 0u);
+            }
+            go = go && n.w != 0u;
+            rec2[(size_t)h * E + e] = n;
+            cur = n;
+        }
     }
 }
 
@@ -260,7 +273,7 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
 }
 
 __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
-                                                  const uint4 *__restrict__ erec2, uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
+                                                  const uint4 *__restrict__ erec2, uint32_t E, uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
                                                   uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
                                                   uint32_t *__restrict__ err, bool pk) {
     const uint32_t lane = threadIdx.x & 63;
@@ -279,9 +292,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
     uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0, eb = 0;  // eb: first edge of u
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     // deferred pushes (see below): entries, offsets, the reserved base (lane 0)
-    bool pend[kLaneEdges + 1];
-    uint32_t pofs[kLaneEdges + 1], pbase = 0, npend = 0;
-    uint64_t pent[kLaneEdges + 1];
+    bool pend[kPush];
+    uint32_t pofs[kPush], pbase = 0, npend = 0;
+    uint64_t pent[kPush];
     uint64_t *pq = Q;
     while (true) {
         // one round: the poll of a claimed slot and one edge step of an item are issued
@@ -338,7 +351,11 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         }
         // per-lane step: up to kLaneEdges edges at once (loads and first CAS attempts all in
         // flight together), so a chain link with a few fan-out children still takes one round
-        bool ready[kLaneEdges], fin_item = false, part = false, skip1 = false;
+        bool ready[kLaneEdges], fin_item = false, part = false;
+        bool jp[kHops - 1];        // a vertex passed by a jump has edges left: queue them (skip 1)
+        uint64_t jent[kHops - 1];
+#pragma unroll
+        for (uint32_t h = 0; h + 1 < kHops; ++h) { jp[h] = false; jent[h] = 0; }
         uint64_t pent_part = 0;
         uint32_t w[kLaneEdges], wl[kLaneEdges];
 #pragma unroll
@@ -348,15 +365,17 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         // shared tail) overlaps the record load instead of preceding it -- on a chain the two
         // were serial round trips per hop
         const uint32_t ne = has_item ? min(e1 - e, kLaneEdges) : 0u;
-        uint4 erv[kLaneEdges], erv2 = make_uint4(0u, 0u, 0u, 0u);
+        uint4 erv[kLaneEdges], erh[kHops - 1];
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k)
             if (k < ne) erv[k] = erec[e + k];
-        if (pk && ne) erv2 = erec2[e];  // the hop after edge e (two-level jump, k_edge_rec)
+#pragma unroll
+        for (uint32_t h = 0; h + 1 < kHops; ++h)  // the hops after edge e (k_edge_rec), same round trip
+            erh[h] = (pk && ne) ? erec2[(size_t)h * E + e] : make_uint4(0u, 0u, 0u, 0u);
         if (npend) {
             const uint32_t base = __shfl(pbase, 0);
 #pragma unroll
-            for (uint32_t k = 0; k <= kLaneEdges; ++k)
+            for (uint32_t k = 0; k < kPush; ++k)
                 if (pend[k]) __hip_atomic_store(&pq[base + pofs[k]], pent[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             npend = 0;
         }
@@ -405,14 +424,21 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                             // its first dependent w2 ready through w alone -- w is final here,
                             // the lane continues at w2, and w's other edges (if any) are queued
                             // as a partial item skipping the first
-                            if (k == 0 && only[0] && erv2.w != 0u && pk) {
-                                level[cw] = cl;
-                                my_max = max(my_max, cl);
-                                if (ce + 1u < ce1) {
-                                    ready[0] = true;
-                                    skip1 = true;
+                            if (k == 0 && only[0] && pk) {
+                                bool go = true;
+#pragma unroll
+                                for (uint32_t h = 0; h + 1 < kHops; ++h) {
+                                    go = go && erh[h].w != 0u;
+                                    if (go) {
+                                        level[cw] = cl;
+                                        my_max = max(my_max, cl);
+                                        if (ce + 1u < ce1) {
+                                            jp[h] = true;
+                                            jent[h] = ((uint64_t)((cl << 8) | 1u) << 32) | cw;
+                                        }
+                                        cw = erh[h].x; cl = cl + 1u; ce = erh[h].y; ce1 = erh[h].z;
+                                    }
                                 }
-                                cw = erv2.x; cl = cl + 1u; ce = erv2.y; ce1 = erv2.z;
                             }
                         } else {
                             ready[k] = true;
@@ -471,26 +497,38 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         // pushes, deferred by one round: this round reserves the queue slots (the add's
         // result is not waited for), the next round stores the entries -- the reservation's
         // round trip overlaps the next round's loads instead of adding to this one
-        uint64_t rm[kLaneEdges + 1];
-        uint32_t tot = 0;
+        // entries: [0, kLaneEdges) ready children, then the jumps' partial items, then u's part
+        bool pp[kPush];
+        uint64_t pe[kPush];
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k) {
-            rm[k] = __ballot(ready[k]);
+            pp[k] = ready[k];
+            pe[k] = ((uint64_t)(pk ? wl[k] << 8 : wl[k]) << 32) | w[k];
+        }
+#pragma unroll
+        for (uint32_t h = 0; h + 1 < kHops; ++h) {
+            pp[kLaneEdges + h] = jp[h];
+            pe[kLaneEdges + h] = jent[h];
+        }
+        pp[kPush - 1] = part;
+        pe[kPush - 1] = pent_part;
+        uint64_t rm[kPush];
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPush; ++k) {
+            rm[k] = __ballot(pp[k]);
             tot += (uint32_t)__popcll(rm[k]);
         }
-        rm[kLaneEdges] = __ballot(part);
-        tot += (uint32_t)__popcll(rm[kLaneEdges]);
         if (tot) {
             const uint32_t ps = (sh + ++rr) % kShards;
             if (lane == 0) pbase = atomicAdd(&ctl[(kShards + ps) * kCtlStride], tot);
             pq = Q + (size_t)ps * V;
             uint32_t run = 0;
 #pragma unroll
-            for (uint32_t k = 0; k <= kLaneEdges; ++k) {
-                pend[k] = k < kLaneEdges ? ready[k] : part;
+            for (uint32_t k = 0; k < kPush; ++k) {
+                pend[k] = pp[k];
                 pofs[k] = run + (uint32_t)__popcll(rm[k] & lt);
-                pent[k] = k < kLaneEdges ? ((uint64_t)(pk ? (wl[k] << 8) | (k == 0 && skip1 ? 1u : 0u) : wl[k]) << 32) | w[k]
-                                         : pent_part;
+                pent[k] = pe[k];
                 run += (uint32_t)__popcll(rm[k]);
             }
             npend = 1;
@@ -595,7 +633,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     // cnt[L] = frontier size of level L (one counter per possible level: <= V + 1)
     const size_t ncnt = (size_t)V + 2;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + (size_t)V * 8 * (1 + kShards) +
-                                   (size_t)E * 32 + kCtlWords * 4 + 22 * 256);  // erec + erec2
+                                   (size_t)E * 16 * kHops + kCtlWords * 4 + 22 * 256);  // erec + erec2
     if (rc) return rc;
     fp_ws_reset(c);
     uint32_t *indeg = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
@@ -629,7 +667,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         uint64_t *Q = (uint64_t *)fp_ws_take(c, (size_t)V * 8 * kShards);
         uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
         uint4 *erec = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
-        uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
+        uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16 * (kHops - 1)) : nullptr;
         if (!state || !Q || !actl || (E && (!erec || !erec2))) return FP_ENOMEM;
         FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
         FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
@@ -645,7 +683,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
                                                                                             indeg, erec, erec2);
             FP_HIP(hipGetLastError());
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
-            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, erec2, V, state, Q, actl, level, c->d_err, pk);
+            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err, pk);
             FP_HIP(hipGetLastError());
         }
         FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &actl[26 * kCtlStride], 4, hipMemcpyDeviceToHost, st));
