@@ -218,29 +218,29 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // and the rest of each passed vertex's edges goes to the queue as a partial item.  A chain of
 // depth D takes ~D / kHops rounds.  (Two levels per round: config-5 levelize 1.51 -> 1.13 ms.)
 __global__ void k_edge_rec(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t E,
-                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec,
-                           uint4 *__restrict__ rec2) {
+                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec) {
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t w = col[e];
-        uint4 r = make_uint4(w, 0u, 0u, 0u);
-        bool go = false;
-        if (w < V) {  // else corrupt: k_indeg raised FP_ECORRUPT, no expansion runs
-            r = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
-            go = true;
+        rec[e] = w < V ? make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u)
+                       : make_uint4(w, 0u, 0u, 0u);  // corrupt: k_indeg raised FP_ECORRUPT, no expansion runs
+    }
+}
+
+// Hop h + 1 of every edge by pointer jumping over the finished records: the hop after edge e's
+// child w is the record of w's first edge (rec[rec[e].y]), and hop h + 1 of e is hop h of that
+// first edge -- one dependent 16-B load per edge and hop, instead of chasing col / row_ptr.
+// A hop is kept only while every edge before it is an only-parent edge (zero record otherwise).
+__global__ void k_edge_hop(uint32_t E, const uint4 *__restrict__ rec, const uint4 *__restrict__ prev,
+                           uint4 *__restrict__ next) {
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint4 r = rec[e];
+        const uint4 p = prev ? prev[e] : r;  // the hop before (the child itself for the first hop)
+        uint4 n = make_uint4(0u, 0u, 0u, 0u);
+        if (p.w != 0u && r.w != 0u && r.z > r.y && r.y < E) {
+            const uint4 f = prev ? prev[r.y] : rec[r.y];  // hop (h) of the child's first edge
+            if (f.w != 0u) n = f;
         }
-        rec[e] = r;
-        uint4 cur = r;
-#pragma unroll
-        for (uint32_t h = 0; h + 1 < kHops; ++h) {
-            uint4 n = make_uint4(0u, 0u, 0u, 0u);
-            if (go && cur.z > cur.y) {
-                const uint32_t w2 = col[cur.y];
-                if (w2 < V) n = make_uint4(w2, row_ptr[w2], row_ptr[w2 + 1], indeg[w2] == 1u ? 1u : 0u);
-            }
-            go = go && n.w != 0u;
-            rec2[(size_t)h * E + e] = n;
-            cur = n;
-        }
+        next[e] = n;
     }
 }
 
@@ -679,9 +679,13 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         // a corrupt CSR (k_check_csr / k_indeg) stops here, before any expansion
         if ((rc = fp_take_err(c))) return rc;
         if (E) {
-            k_edge_rec<<<blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192, 256, 0, st>>>(g->row_ptr, g->col, E, V,
-                                                                                            indeg, erec, erec2);
+            const unsigned eg = blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192;
+            k_edge_rec<<<eg, 256, 0, st>>>(g->row_ptr, g->col, E, V, indeg, erec);
             FP_HIP(hipGetLastError());
+            for (uint32_t h = 0; h + 1 < kHops; ++h) {
+                k_edge_hop<<<eg, 256, 0, st>>>(E, erec, h ? erec2 + (size_t)(h - 1) * E : nullptr, erec2 + (size_t)h * E);
+                FP_HIP(hipGetLastError());
+            }
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
             k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err, pk);
             FP_HIP(hipGetLastError());

@@ -9,3 +9,4 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
 tail -1 gpurun_out/${tag}_tests.log
 timeout -k 10 200 python -u tools/lvl_time.py > gpurun_out/${tag}_lvl.jsonl 2>&1 || { echo "lvl failed"; tail gpurun_out/${tag}_lvl.jsonl; exit 1; }
 cat gpurun_out/${tag}_lvl.jsonl
+bash tools/gpu_r03t.sh
