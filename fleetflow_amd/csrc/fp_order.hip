@@ -585,6 +585,103 @@ __global__ void k_lvl_async_final(uint32_t V, uint32_t cyc_key, const uint32_t *
     if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(ncyc, (uint32_t)__popcll(m));
 }
 
+// ---- stable counting sort of the level keys (the start order) ----------------------------
+// keys[v] < nb <= CS_BINS, order = stable sort of 0..V-1 by key.  Three small launches instead
+// of rocprim's ~21 radix passes (launch-bound at config 5's 1M keys: 0.16 ms):
+//   k_cs_hist    per tile of CS_TILE keys: a histogram in LDS -> hist[tile][bin]
+//   k_cs_scan    one workgroup: hist[tile][bin] <- bin base + keys of the bin in earlier tiles
+//   k_cs_scatter per tile: per-wave counts of each wave's contiguous slice, then each wave walks
+//                its slice in order, 64 keys at a time, ranking equal keys by a ballot match mask
+//                (the same stable scheme as fp_place.hip's per-scenario sort)
+constexpr uint32_t CS_TILE = 16384, CS_BINS = 1024, CS_WAVES = 16, CS_MAX_TILES = 1024;
+__global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t nb,
+                                                  uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[CS_BINS];
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
+    for (uint32_t i = threadIdx.x; i < CS_TILE && t0 + i < V; i += blockDim.x) atomicAdd(&h[min(keys[t0 + i], nb - 1)], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[(size_t)blockIdx.x * nb + b] = h[b];
+}
+
+__global__ __launch_bounds__(1024) void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t nb) {
+    __shared__ uint32_t tot[CS_BINS];
+    const uint32_t b = threadIdx.x;  // one bin per thread (nb <= CS_BINS = blockDim)
+    uint32_t run = 0;
+    if (b < nb)
+        for (uint32_t t0 = 0; t0 < ntiles; t0 += 8) {  // 8 independent loads in flight
+            uint32_t x[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) x[j] = t0 + j < ntiles ? hist[(size_t)(t0 + j) * nb + b] : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j)
+                if (t0 + j < ntiles) {
+                    hist[(size_t)(t0 + j) * nb + b] = run;
+                    run += x[j];
+                }
+        }
+    tot[b] = b < nb ? run : 0u;
+    __syncthreads();
+    // exclusive scan of tot[] (Hillis-Steele in LDS)
+    for (uint32_t o = 1; o < CS_BINS; o <<= 1) {
+        const uint32_t y = b >= o ? tot[b - o] : 0u;
+        __syncthreads();
+        tot[b] += y;
+        __syncthreads();
+    }
+    const uint32_t base = tot[b] - run;  // inclusive - own
+    if (b < nb)
+        for (uint32_t t = 0; t < ntiles; ++t) hist[(size_t)t * nb + b] += base;
+}
+
+__device__ __forceinline__ uint64_t cs_match(uint32_t v, bool valid, uint32_t nbits) {
+    uint64_t m = __builtin_amdgcn_ballot_w64(valid);
+    for (uint32_t i = 0; i < nbits; ++i) {
+        const bool bit = (v >> i) & 1u;
+        const uint64_t bb = __builtin_amdgcn_ballot_w64(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict__ keys, uint32_t V, uint32_t nb,
+                                                     uint32_t nbits, const uint32_t *__restrict__ off,
+                                                     uint32_t *__restrict__ order) {
+    __shared__ uint32_t wh[CS_WAVES][CS_BINS];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t i = t; i < CS_WAVES * CS_BINS; i += blockDim.x) (&wh[0][0])[i] = 0;
+    __syncthreads();
+    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
+    const uint32_t slice = CS_TILE / CS_WAVES;
+    const size_t s0 = t0 + (size_t)w * slice;
+    for (uint32_t i = lane; i < slice && s0 + i < V; i += 64) atomicAdd(&wh[w][min(keys[s0 + i], nb - 1)], 1u);
+    __syncthreads();
+    for (uint32_t b = t; b < nb; b += blockDim.x) {  // per bin: wave offsets in wave order
+        uint32_t run = off[(size_t)blockIdx.x * nb + b];
+        for (uint32_t ww = 0; ww < CS_WAVES; ++ww) {
+            const uint32_t x = wh[ww][b];
+            wh[ww][b] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < slice && s0 + i0 < V; i0 += 64) {
+        const size_t v = s0 + i0 + lane;
+        const bool valid = i0 + lane < slice && v < V;
+        const uint32_t k = valid ? min(keys[v], nb - 1) : 0u;
+        const uint64_t m = cs_match(k, valid, nbits);
+        const uint32_t o = wh[w][k];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane's read before the update
+        if (valid) {
+            if ((m & lt) == 0) wh[w][k] = o + (uint32_t)__popcll(m);
+            order[o + (uint32_t)__popcll(m & lt)] = (uint32_t)v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
 inline unsigned blocks_for(size_t n, unsigned b) {
     size_t g = (n + b - 1) / b;
     return (unsigned)(g ? g : 1);
@@ -616,6 +713,27 @@ int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
     return FP_OK;
 }
 
+// order = stable sort of 0..V-1 by keys[] (keys <= cyc_key): the counting sort above when the
+// keys fit its bins and tiles, rocprim's radix sort otherwise (or with FP_LVL_RADIX_SORT set).
+static int level_sort(hipStream_t st, uint32_t *keys, uint32_t *keys_out, uint32_t *vals, uint32_t *order, uint32_t V,
+                      uint32_t cyc_key, void *tmp, size_t sort_tmp, uint32_t *cs_hist) {
+    const uint32_t nb = cyc_key + 1;
+    const uint32_t ntiles = (uint32_t)(((size_t)V + CS_TILE - 1) / CS_TILE);
+    static const bool force_radix = getenv("FP_LVL_RADIX_SORT") != nullptr;
+    if (!force_radix && nb <= CS_BINS && ntiles <= CS_MAX_TILES) {
+        k_cs_hist<<<ntiles, 1024, 0, st>>>(keys, V, nb, cs_hist);
+        FP_HIP(hipGetLastError());
+        k_cs_scan<<<1, CS_BINS, 0, st>>>(cs_hist, ntiles, nb);
+        FP_HIP(hipGetLastError());
+        k_cs_scatter<<<ntiles, 1024, 0, st>>>(keys, V, nb, fp_bitwidth(cyc_key), cs_hist, order);
+        FP_HIP(hipGetLastError());
+        return FP_OK;
+    }
+    FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys, keys_out, vals, order, (size_t)V, 0, fp_bitwidth(cyc_key),
+                                     st));
+    return FP_OK;
+}
+
 int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t *order,
                          uint32_t *n_cycle_dev) {
     const uint32_t V = g->n_vertices, E = g->n_edges;
@@ -633,7 +751,8 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     // cnt[L] = frontier size of level L (one counter per possible level: <= V + 1)
     const size_t ncnt = (size_t)V + 2;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + (size_t)V * 8 * (1 + kShards) +
-                                   (size_t)E * 16 * kHops + kCtlWords * 4 + 22 * 256);  // erec + erec2
+                                   (size_t)E * 16 * kHops + kCtlWords * 4 + (size_t)CS_MAX_TILES * CS_BINS * 4 +
+                                   23 * 256);  // erec + hops, counting-sort histograms
     if (rc) return rc;
     fp_ws_reset(c);
     uint32_t *indeg = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
@@ -645,7 +764,8 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     uint32_t *cnt = (uint32_t *)fp_ws_take(c, ncnt * 4);
     uint32_t *ncyc = (uint32_t *)fp_ws_take(c, 64);
     void *tmp = fp_ws_take(c, sort_tmp + 16);
-    if (!indeg || !fa || !fb || !keys || !keys_out || !vals || !cnt || !ncyc || !tmp) return FP_ENOMEM;
+    uint32_t *cs_hist = (uint32_t *)fp_ws_take(c, (size_t)CS_MAX_TILES * CS_BINS * 4);
+    if (!indeg || !fa || !fb || !keys || !keys_out || !vals || !cnt || !ncyc || !tmp || !cs_hist) return FP_ENOMEM;
 
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_LEVEL, &ev);
@@ -697,8 +817,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
         k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, cyc_key, level, keys, vals, ncyc);
         FP_HIP(hipGetLastError());
-        FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys, keys_out, vals, order, (size_t)V, 0,
-                                         fp_bitwidth(cyc_key), st));
+        if ((rc = level_sort(st, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
         if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
@@ -733,8 +852,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     const uint32_t cyc_key = iters + 2;
     k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, ncyc);
     FP_HIP(hipGetLastError());
-    FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys, keys_out, vals, order, (size_t)V, 0,
-                                     fp_bitwidth(cyc_key), st));
+    if ((rc = level_sort(st, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
     if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
     fp_prof_end(c, FP_K_LEVEL, ev);
     return FP_OK;
