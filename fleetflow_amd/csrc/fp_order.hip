@@ -714,13 +714,12 @@ int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
 }
 
 // order = stable sort of 0..V-1 by keys[] (keys <= cyc_key): the counting sort above when the
-// keys fit its bins and tiles, rocprim's radix sort otherwise (or with FP_LVL_RADIX_SORT set).
-static int level_sort(hipStream_t st, uint32_t *keys, uint32_t *keys_out, uint32_t *vals, uint32_t *order, uint32_t V,
+// keys fit its bins and tiles, rocprim's radix sort otherwise (or with FP_OPT_LEVEL_SORT = 0).
+static int level_sort(hipStream_t st, bool counting, uint32_t *keys, uint32_t *keys_out, uint32_t *vals, uint32_t *order, uint32_t V,
                       uint32_t cyc_key, void *tmp, size_t sort_tmp, uint32_t *cs_hist) {
     const uint32_t nb = cyc_key + 1;
     const uint32_t ntiles = (uint32_t)(((size_t)V + CS_TILE - 1) / CS_TILE);
-    static const bool force_radix = getenv("FP_LVL_RADIX_SORT") != nullptr;
-    if (!force_radix && nb <= CS_BINS && ntiles <= CS_MAX_TILES) {
+    if (counting && nb <= CS_BINS && ntiles <= CS_MAX_TILES) {
         k_cs_hist<<<ntiles, 1024, 0, st>>>(keys, V, nb, cs_hist);
         FP_HIP(hipGetLastError());
         k_cs_scan<<<1, CS_BINS, 0, st>>>(cs_hist, ntiles, nb);
@@ -817,7 +816,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
         k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, cyc_key, level, keys, vals, ncyc);
         FP_HIP(hipGetLastError());
-        if ((rc = level_sort(st, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
+        if ((rc = level_sort(st, fp_opt(c, FP_OPT_LEVEL_SORT, 1) != 0, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
         if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
@@ -852,7 +851,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     const uint32_t cyc_key = iters + 2;
     k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, ncyc);
     FP_HIP(hipGetLastError());
-    if ((rc = level_sort(st, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
+    if ((rc = level_sort(st, fp_opt(c, FP_OPT_LEVEL_SORT, 1) != 0, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
     if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
     fp_prof_end(c, FP_K_LEVEL, ev);
     return FP_OK;

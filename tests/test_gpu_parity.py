@@ -97,6 +97,34 @@ def test_levelize_async_shapes(shape, planner, O):
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
+@pytest.mark.parametrize("sync,sort", [(0, 1), (1, 1), (0, 0)])
+@pytest.mark.parametrize("chain", [1022, 1023, 1024, 1025])
+def test_levelize_start_order_sort_limits(chain, sync, sort, planner, O):
+    """The start order's counting sort (fp_order.hip `level_sort`) takes at most 1024 keys
+    (levels + the cycle key); longer graphs take the radix sort.  Chains around that limit,
+    over 19 ragged counting-sort tiles with side edges, a 3-cycle, both schedules, and the
+    radix sort forced (FP_OPT_LEVEL_SORT = 0)."""
+    rng = np.random.default_rng(chain)
+    V = 300_001
+    edges = [(v, v + 1) for v in range(chain - 1)]
+    a, b = rng.integers(0, V, 60_000), rng.integers(0, V, 60_000)
+    edges += [(int(x), int(y)) for x, y in zip(a, b) if chain <= x < y]  # max level = chain - 1 exactly
+    edges += [(V - 3, V - 2), (V - 2, V - 1), (V - 1, V - 3)]
+    rp, col = _csr(V, edges)
+    hd = np.zeros(V, np.uint8)
+    hd[np.unique(col)] = 1
+    planner.set_option("levelize_sync", sync)
+    planner.set_option("level_sort", sort)
+    try:
+        level, order, ncyc = planner.levelize(rp, col, hd)
+    finally:
+        planner.set_option("levelize_sync")
+        planner.set_option("level_sort")
+    el, eo, en = O.levelize(rp, col, hd)
+    assert en >= 3
+    assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
 def test_levelize_async_unpacked_entries(planner, O):
     """V >= 2^24: queue entries cannot pack (level << 8 | skip), so the asynchronous
     levelizer runs without partial hand-off (fp_order.hip `pk`); same levels and order."""

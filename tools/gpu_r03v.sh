@@ -1,6 +1,6 @@
 #!/bin/bash
 # Levelizer counting-sort check: levelizer parity tests, then config-5 levelize time with the
-# counting sort and with rocprim's radix sort (FP_LVL_RADIX_SORT=1) in one call, then the trace.
+# counting sort and with rocprim's radix sort (level_sort=0) in one call, then the trace.
 set -o pipefail
 root=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$root" || exit 1
@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
 tail -1 gpurun_out/${tag}_tests.log
 timeout -k 10 200 python -u tools/lvl_time.py > gpurun_out/${tag}_lvl.jsonl 2>&1 || { echo "lvl failed"; tail gpurun_out/${tag}_lvl.jsonl; exit 1; }
 echo "counting sort"; cat gpurun_out/${tag}_lvl.jsonl
-FP_LVL_RADIX_SORT=1 timeout -k 10 200 python -u tools/lvl_time.py > gpurun_out/${tag}_lvl_radix.jsonl 2>&1 || { echo "lvl radix failed"; tail gpurun_out/${tag}_lvl_radix.jsonl; exit 1; }
+timeout -k 10 200 python -u tools/lvl_time.py level_sort=0 > gpurun_out/${tag}_lvl_radix.jsonl 2>&1 || { echo "lvl radix failed"; tail gpurun_out/${tag}_lvl_radix.jsonl; exit 1; }
 echo "radix sort"; cat gpurun_out/${tag}_lvl_radix.jsonl
 timeout -k 10 300 python -u tools/lvl_time.py > gpurun_out/${tag}_lvl2.jsonl 2>&1 || exit 1
 echo "counting sort again"; cat gpurun_out/${tag}_lvl2.jsonl

@@ -1,4 +1,5 @@
-"""Config-5 levelization timing (bench.py's levelize_leg, kernel and wall ms) on cuda:0."""
+"""Config-5 levelization timing (bench.py's levelize_leg, kernel and wall ms) on cuda:0.
+    python tools/lvl_time.py [option=value ...]   (context options, _lib.OPTIONS names)"""
 import json
 import os
 import sys
@@ -12,6 +13,9 @@ import bench  # noqa: E402
 from fleetflow_amd import Planner  # noqa: E402
 
 with Planner(0) as p:
+    for kv in sys.argv[1:]:
+        k, v = kv.split("=")
+        p.set_option(k, int(v))
     for _ in range(2):
         lv, _, _, _ = bench.levelize_leg(p, torch.device("cuda", 0), 10)
         print(json.dumps({k: lv[k] for k in ("ms_per_step", "kernel_ms", "levels", "cycle_vertices")}), flush=True)
