@@ -352,6 +352,22 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
 // FP_WIDE12_WAVES waves per SIMD: 5 fits them in 96 VGPRs (32 B of scratch) and 20 segments per
 // CU -- config-4 FFD 20.9 -> 18.7 ms against the 1024-thread kernel's 107 VGPRs and four waves
 // (6 waves: 80 VGPRs, 100 B of scratch, 19.2 ms).  0 selects the 1024-thread kernel.
+// Batch prescan: skip a group's bucket-mask loads when its corner is empty, in the wide stages
+// (config-4 FFD 17.38 -> 15.72 ms; a batch that passes a segment mostly has every corner empty).
+// The narrow stages keep the branch-free form (config 3: 64.3 vs 65.3 ms with the skip).
+// (r03z A/B, profiles/r03z_prescan_ab.jsonl)
+#ifndef FP_PRESCAN_SKIP_WIDE
+#define FP_PRESCAN_SKIP_WIDE 1
+#endif
+#ifndef FP_PRESCAN_SKIP_NARROW
+#define FP_PRESCAN_SKIP_NARROW 0
+#endif
+// skip the group loop when no container of the batch has a candidate group (config-4 FFD
+// 15.62 -> 15.06 ms, config 3 64.3 -> 63.6 ms;
+// profiles/r03aa_todo_ab.jsonl, r03ab_todo_ab.jsonl)
+#ifndef FP_TODO_SKIP
+#define FP_TODO_SKIP 1
+#endif
 #ifndef FP_WIDE12_WAVES
 #define FP_WIDE12_WAVES 5
 #endif
@@ -633,12 +649,19 @@ k_ffd_pipe(const PipeArgs a) {
         const uint32_t qm = wave_min(valid ? mem : 0xFFFFFFFFu);
         // every mask load is issued before the first use (no per-group LDS round trip)
         const uint32_t oc = kc * 2, om = km * 2 + 1;
+        constexpr bool prescan_skip = G > FP_SYS_MAX_G ? FP_PRESCAN_SKIP_WIDE : FP_PRESCAN_SKIP_NARROW;
         GM cand = 0;
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
             const uint64_t e = __builtin_amdgcn_ballot_w64((rcf[g] >= qc) & (rmf[g] >= qm));
             const uint64_t *mg = Mw + (size_t)g * K * 2;
-            cand |= (mg[oc] & mg[om] & e) ? GM(1) << g : GM(0);
+            if (prescan_skip) {
+                // a group whose corner is empty fits no container of the batch: no mask loads
+                // (most wide-stage batches pass through with every corner empty)
+                if (e) cand |= (mg[oc] & mg[om] & e) ? GM(1) << g : GM(0);
+            } else {
+                cand |= (mg[oc] & mg[om] & e) ? GM(1) << g : GM(0);
+            }
         }
         cand = valid ? cand : GM(0);
         const bool zero = valid && (cpu | mem | req | conf) == 0u;
@@ -782,6 +805,7 @@ k_ffd_pipe(const PipeArgs a) {
             // exact: a stale mask is a superset): config 3 (1 x 1M x 100k) ran 127 -> 104 ms
             // without the update, while config 4's 20-group stages need it (57 vs 66 ms)
             uint32_t nchk = 0, nhit = 0;
+            if (!FP_TODO_SKIP || todo)
             fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                    used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                    (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
