@@ -365,6 +365,12 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
 // skip the group loop when no container of the batch has a candidate group (config-4 FFD
 // 15.62 -> 15.06 ms, config 3 64.3 -> 63.6 ms;
 // profiles/r03aa_todo_ab.jsonl, r03ab_todo_ab.jsonl)
+// A/B variant: req / conf of link input loaded after the prescan, only for batches with a
+// candidate.  Slower (config-4 FFD 15.45 vs 15.08 ms, profiles/r03ac_defer_ab.jsonl): the kernel
+// is issue-bound, and a batch with a candidate then waits on a second load round trip.
+#ifndef FP_DEFER_RC
+#define FP_DEFER_RC 0
+#endif
 #ifndef FP_TODO_SKIP
 #define FP_TODO_SKIP 1
 #endif
@@ -481,6 +487,9 @@ k_ffd_pipe(const PipeArgs a) {
     __syncthreads();
 
     const bool has_out = w + 1 < W;
+    // a global-link consumer that forwards positions only (the segment's last stage) loads a
+    // container's req / conf after the prescan, when the batch has a candidate here
+    const bool defer_rc = FP_DEFER_RC && !has_out;
     const bool g_in = w == 0 && b > 0;                  // input from segment b-1
     const bool g_out = w + 1 == W && b + 1 < B;         // output to segment b+1
     // a global link slot: [0] = count (or END), [64..127] = the containers' FFD positions;
@@ -567,8 +576,10 @@ k_ffd_pipe(const PipeArgs a) {
                 const uint32_t p = pos & pmask;
                 cpu = a.s_cpu[cb + p];
                 mem = a.s_mem[cb + p];
-                req = a.s_req[cb + p];
-                conf = a.s_conf[cb + p];
+                if (!defer_rc) {
+                    req = a.s_req[cb + p];
+                    conf = a.s_conf[cb + p];
+                }
             }
             itail++;
         } else if (w == 0) {
@@ -664,6 +675,14 @@ k_ffd_pipe(const PipeArgs a) {
             }
         }
         cand = valid ? cand : GM(0);
+        if (defer_rc && g_in && (__builtin_amdgcn_ballot_w64(cand != 0) != 0 || (qc | qm) == 0u)) {
+            // labels and conflicts, needed only when some container has a candidate group (or a
+            // zero demand: then qc = qm = 0).  A batch that passes the segment forwards positions.
+            if (valid) {
+                req = a.s_req[cb + (idx & pmask)];
+                conf = a.s_conf[cb + (idx & pmask)];
+            }
+        }
         const bool zero = valid && (cpu | mem | req | conf) == 0u;
         uint64_t todo = __builtin_amdgcn_ballot_w64(cand != 0 && !zero);
         uint64_t placed = 0;
