@@ -184,6 +184,16 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 constexpr size_t LCTL = 64;  // u32 per global link control block: [0] head, [LCTL / 2] tail
 
 // Bounded global link: wait (wave-uniform) until the producer may write every slot below
@@ -272,13 +282,13 @@ using RecT = uint32_t[G];
 #define FP_GROUP_LOOP fpp_group_x
 #endif
 #define FPP_GROUP_LOOP FP_GROUP_LOOP
-template <uint32_t G, bool UPD, uint32_t... gs, class Rec>
+template <uint32_t G, bool UPD, bool GB, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
-                                           uint32_t &nhit, uint32_t sys) {
+                                           uint32_t &nhit, uint32_t sys, uint32_t &gmc, uint32_t &gmm) {
     constexpr uint32_t pf_max = G <= FP_SYS_MAX_G ? FP_PF_MAX_NARROW : FP_PF_MAX_WIDE;
     (
         [&] {
@@ -316,6 +326,11 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                     FPP_GROUP_LOOP<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                          req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
                 if (touched) {
+                    if (GB) {  // the group's bounds (largest free cpu / mem) after its placements
+                        const uint32_t xc = wave_max(rcf[gs]), xm = wave_max(rmf[gs]);
+                        gmc = lane == gs ? xc : gmc;
+                        gmm = lane == gs ? xm : gmm;
+                    }
                     const bool me = (touched >> lane) & 1ull;
                     if (gs < 32) used |= me ? (1u << gs) : 0u;
                     else used_hi |= me ? (1u << (gs & 31)) : 0u;
@@ -361,6 +376,12 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
 #endif
 #ifndef FP_PRESCAN_SKIP_NARROW
 #define FP_PRESCAN_SKIP_NARROW 0
+#endif
+// A/B variant: per-group bounds of the largest free cpu / mem skip the corner ballots.  Slower
+// (config-4 FFD 15.73 vs 15.08 ms, profiles/r03af_bound_ab.jsonl): the bounds' upkeep after a
+// group's placements costs more than the ballots they save.
+#ifndef FP_GROUP_BOUND
+#define FP_GROUP_BOUND 0
 #endif
 // skip the group loop when no container of the batch has a candidate group (config-4 FFD
 // 15.62 -> 15.06 ms, config 3 64.3 -> 63.6 ms;
@@ -466,6 +487,19 @@ k_ffd_pipe(const PipeArgs a) {
         if (zs_g == G && sm) {
             zs_g = g;
             zs_l = (uint32_t)__builtin_ctzll(sm);
+        }
+    }
+    // group bounds (wide stages, FP_GROUP_BOUND): lane g holds an upper bound of group g's largest
+    // free cpu / mem.  Free capacity only shrinks, so a stale bound stays an upper bound; groups
+    // whose bounds are below the batch corner skip the exact corner ballot.
+    constexpr bool gbound = FP_GROUP_BOUND && G > FP_SYS_MAX_G && G <= 64;
+    uint32_t gmc = 0, gmm = 0;
+    if (gbound) {
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t xc = wave_max(rcf[g]), xm = wave_max(rmf[g]);
+            gmc = lane == g ? xc : gmc;
+            gmm = lane == g ? xm : gmm;
         }
     }
     // bucket-major (a rolled loop): two thresholds live in scalars at a time -- hoisting all
@@ -662,8 +696,10 @@ k_ffd_pipe(const PipeArgs a) {
         const uint32_t oc = kc * 2, om = km * 2 + 1;
         constexpr bool prescan_skip = G > FP_SYS_MAX_G ? FP_PRESCAN_SKIP_WIDE : FP_PRESCAN_SKIP_NARROW;
         GM cand = 0;
+        const uint64_t galive = gbound ? __builtin_amdgcn_ballot_w64((gmc >= qc) & (gmm >= qm)) : ~0ull;
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
+            if (gbound && !((galive >> g) & 1ull)) continue;  // no node of g reaches the corner
             const uint64_t e = __builtin_amdgcn_ballot_w64((rcf[g] >= qc) & (rmf[g] >= qm));
             const uint64_t *mg = Mw + (size_t)g * K * 2;
             if (prescan_skip) {
@@ -825,10 +861,10 @@ k_ffd_pipe(const PipeArgs a) {
             // without the update, while config 4's 20-group stages need it (57 vs 66 ms)
             uint32_t nchk = 0, nhit = 0;
             if (!FP_TODO_SKIP || todo)
-            fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+            fpp_groups<G, (G > 1), gbound>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                    used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                    (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
-                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys);
+                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gmc, gmm);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
 #else
 #pragma unroll
