@@ -1845,6 +1845,18 @@ extern "C" int fp_debug_clock_ghz(fp_ctx *c, double *ghz) {
     *ghz = (double)h[0] / (double)h[1] * 0.1;
     return FP_OK;
 }
+#ifdef FP_PIPE_STATS
+extern "C" int fp_debug_sys_stats(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sys_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+        return FP_EDEVICE;
+    if (reset) {
+        static const unsigned long long zero[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sys_stats), zero, sizeof(zero)) != hipSuccess) return FP_EDEVICE;
+    }
+    return FP_OK;
+}
+#endif
+
 extern "C" int fp_debug_pipe_stats(unsigned long long *out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_stats), sizeof(unsigned long long) * 16 * 16) != hipSuccess)
         return FP_EDEVICE;

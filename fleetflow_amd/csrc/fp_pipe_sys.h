@@ -27,6 +27,13 @@
 
 namespace fpp {
 
+#ifdef FP_PIPE_STATS
+// systolic-call diagnostics (stats build): [0] calls [1] queued Q [2] live L [3] steps [4] placed
+// [5] live nodes that fit at least one queued container (2-D + labels/conflicts, batch-start state)
+// [6] largest placement position + 1, summed over calls
+__device__ unsigned long long g_sys_stats[8];
+#endif
+
 // DPP wave_ror:1 -- lane i receives lane i-1, lane 0 receives lane 63
 __device__ __forceinline__ uint32_t sys_ror1(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x13C, 0xF, 0xF, false);
@@ -46,6 +53,38 @@ __device__ __forceinline__ uint32_t sys_wave_or(uint32_t x) {
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+#ifndef FP_SYS_STAIR
+#define FP_SYS_STAIR 0
+#endif
+// The live nodes that dominate some queued container in (cpu, mem) -- the queue's staircase.
+// Queued lanes hold non-increasing cpu (FFD order); lane t is a staircase point when its mem is
+// below every later queued lane's.  Every queued container is dominated by a staircase point at or
+// after it (the last lane holding the minimum mem of its suffix), so a node outside the result fits
+// no queued container, now or after any placement: dropping it from the live set is exact.
+__device__ __forceinline__ uint64_t sys_stair(uint64_t q, uint32_t cpu, uint32_t mem, uint32_t rcf, uint32_t rmf) {
+    const uint32_t lane = __lane_id();
+    const uint32_t m = ((q >> lane) & 1ull) ? mem : 0xFFFFFFFFu;
+    // min over the later lanes: reverse the lanes, exclusive prefix min (wave_shr:1, then the row
+    // scan of wave_min), reverse back
+    const uint32_t r = sys_pull(63u - lane, m);
+    uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)r, 0x138, 0xF, 0xF, false);  // wave_shr:1
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x111, 0xF, 0xF, false));      // row_shr:1
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x112, 0xF, 0xF, false));      // row_shr:2
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x114, 0xF, 0xF, false));      // row_shr:4
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x118, 0xF, 0xF, false));      // row_shr:8
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x142, 0xA, 0xF, false));      // row_bcast:15
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x143, 0xC, 0xF, false));      // row_bcast:31
+    const uint32_t later = sys_pull(63u - lane, x);
+    uint64_t pts = __builtin_amdgcn_ballot_w64(((q >> lane) & 1ull) && m < later);
+    bool useful = false;
+    while (pts) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(pts);
+        pts &= pts - 1;
+        useful |= (rcf >= __builtin_amdgcn_readlane(cpu, t)) & (rmf >= __builtin_amdgcn_readlane(mem, t));
+    }
+    return __builtin_amdgcn_ballot_w64(useful);
 }
 
 // One group's queue q (lanes = containers in FFD order; cpu/mem/req/conf per lane) against
@@ -142,7 +181,8 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     SysOut out{0};
     // live nodes: the batch corner (a node outside it fits no container of the batch, now or
     // later) -> positions 0..L-1, in node order
-    const uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
+    uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
+    if (FP_SYS_STAIR && lm) lm &= sys_stair(q, cpu, mem, rcf, rmf);
     const uint32_t L = (uint32_t)__builtin_popcountll(lm);
     if (L == 0) {  // nothing can fit: every queued container misses the group
         if ((q >> lane) & 1ull) asg = 0xFFFFFFFFu;
@@ -195,6 +235,35 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     if (tau >= L && tau - L < 64) pend &= ~(1ull << (tau - L));
 #else
     fpp_sys_steps(xc, xm, xu, xl, kc, km, kr, kx, apos, pend, tau, L, max_steps);
+#endif
+#ifdef FP_PIPE_STATS
+    {
+        // live nodes some queued container fits at the batch-start state (before the steps: the
+        // records below are still the node lanes' own)
+        bool useful = false;
+        uint64_t qq = q;
+        while (qq) {
+            const uint32_t t = (uint32_t)__builtin_ctzll(qq);
+            qq &= qq - 1;
+            const uint32_t c_c = __builtin_amdgcn_readlane(cpu, t), c_m = __builtin_amdgcn_readlane(mem, t);
+            const uint32_t c_r = __builtin_amdgcn_readlane(req, t), c_x = __builtin_amdgcn_readlane(conf, t);
+            useful |= (rcf >= c_c) & (rmf >= c_m) & (((rlab & c_r) | (rcu & c_x)) == 0u);
+        }
+        const uint32_t nu = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(useful && live));
+        const uint32_t maxp = apos != 0xFFFFFFFFu ? ((apos - lane) & 63u) + 1u : 0u;
+        uint32_t mp = maxp;
+        for (uint32_t o = 32; o; o >>= 1) mp = max(mp, (uint32_t)__shfl_xor((int)mp, (int)o));
+        if (lane == 0) {
+            atomicAdd(&g_sys_stats[0], 1ull);
+            atomicAdd(&g_sys_stats[1], (unsigned long long)Q);
+            atomicAdd(&g_sys_stats[2], (unsigned long long)L);
+            atomicAdd(&g_sys_stats[3], (unsigned long long)tau);
+            atomicAdd(&g_sys_stats[5], (unsigned long long)nu);
+            atomicAdd(&g_sys_stats[6], (unsigned long long)mp);
+        }
+        const uint32_t npl = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(apos != 0xFFFFFFFFu));
+        if (lane == 0) atomicAdd(&g_sys_stats[4], (unsigned long long)npl);
+    }
 #endif
     // records back to node lanes: after tau rotations position p is at lane (tau - p) & 63
     const uint32_t src = (tau - pos) & 63u;
