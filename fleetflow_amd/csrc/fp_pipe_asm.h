@@ -327,15 +327,12 @@ __device__ __forceinline__ void fpp_asm_group_x(uint64_t &q, uint64_t &touched, 
 #undef FPP_GX_BODY
 #undef FPP_GX_OPERANDS
 
-// Drop-in for fpp_asm_group (same arguments): the exec-masked loop plus the per-group
-// vector epilogue -- placed bits of the hits, next candidate group of the misses.
-template <uint32_t g, uint32_t G>
-__device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64_t &touched, uint32_t &asg,
-                                            uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
-                                            uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
-                                            uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
-                                            uint32_t &nhit, uint32_t qc, uint32_t qm) {
-    const uint64_t q0 = q;
+// The serial loop over queue q with the re-test after each first miss (FP_REFILTER): see
+// fpp_group_x.  gbg = the group's first node index.
+__device__ __forceinline__ void fpp_refilter_loop(uint64_t q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
+                                                  uint32_t &rmf, uint32_t &rcu, uint32_t rlab, uint32_t cpu,
+                                                  uint32_t mem, uint32_t req, uint32_t conf, uint32_t gbg,
+                                                  uint32_t &nchk, uint32_t qc, uint32_t qm) {
 #if FP_REFILTER
     // Stop at the first miss and re-test the rest of the queue, vector-parallel, against the
     // group's current state: a miss usually means the group just filled up for the batch's
@@ -345,7 +342,7 @@ __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64
     // smallest demands) are broadcast and each queued lane tests its own container; one that
     // fits none of them now never will (monotone).  A large corner, or a re-test that drops
     // nothing, finishes the queue in the plain loop.
-    fpp_asm_group_x<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+    fpp_asm_group_x<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
     while (q) {
         uint64_t e = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
         uint64_t fit = 0;
@@ -363,16 +360,28 @@ __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64
             fit = q;
         }
         if (fit == q) {  // nothing to drop: the rest of the queue in the plain loop
-            fpp_asm_group_x<false>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+            fpp_asm_group_x<false>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
             break;
         }
         q = fit;  // the dropped lanes keep asg = FP_NONE: misses of this group
-        fpp_asm_group_x<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+        fpp_asm_group_x<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
     }
 #else
     (void)qc; (void)qm;
-    fpp_asm_group_x<false>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk);
+    fpp_asm_group_x<false>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
 #endif
+}
+
+// Drop-in for fpp_asm_group (same arguments): the exec-masked loop plus the per-group
+// vector epilogue -- placed bits of the hits, next candidate group of the misses.
+template <uint32_t g, uint32_t G>
+__device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64_t &touched, uint32_t &asg,
+                                            uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
+                                            uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
+                                            uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nchk,
+                                            uint32_t &nhit, uint32_t qc, uint32_t qm) {
+    const uint64_t q0 = q;
+    fpp_refilter_loop(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk, qc, qm);
     q = q0;
     const uint32_t lane = __lane_id();
     const bool inq = (q >> lane) & 1ull;

@@ -55,8 +55,24 @@ __device__ __forceinline__ uint32_t sys_wave_or(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
+// A/B variant (slower: config 3 65.2 vs 64.3 ms, profiles/r03ah_stair_ab.jsonl): the systolic
+// calls' live sets hold 12.5 nodes, 12.0 of them useful (r03ah_systolic_stats.jsonl)
 #ifndef FP_SYS_STAIR
 #define FP_SYS_STAIR 0
+#endif
+// The step loop ends at its first miss (a container that tested every live position): the group
+// is then usually full for the batch's sizes, and the containers still pending go to the serial
+// finish, whose re-test (FP_SYS_LEFT_REFILTER) drops the ones that fit no node any more.
+#ifndef FP_SYS_MISS_EXIT
+#define FP_SYS_MISS_EXIT 0
+#endif
+#ifndef FP_SYS_LEFT_REFILTER
+#define FP_SYS_LEFT_REFILTER 0
+#endif
+#if FP_SYS_MISS_EXIT
+#define FPP_SYS_MISS_TEST "s_bitcmp1_b64 %[pend], %[u]\n\t" "s_cbranch_scc1 .LsysMiss%=\n\t"
+#else
+#define FPP_SYS_MISS_TEST ""
 #endif
 // The live nodes that dominate some queued container in (cpu, mem) -- the queue's staircase.
 // Queued lanes hold non-increasing cpu (FFD order); lane t is a staircase point when its mem is
@@ -138,6 +154,7 @@ __device__ __forceinline__ void fpp_sys_steps(uint32_t &xc, uint32_t &xm, uint32
         "s_cmp_ge_u32 %[tau], %[cap]\n\t"
         "s_cbranch_scc1 .LsysEnd%=\n\t"
         "s_lshl_b64 %[win], %[win], 1\n\t"
+        FPP_SYS_MISS_TEST
         "s_bitset0_b64 %[pend], %[u]\n\t"
         "s_add_u32 %[u], %[u], 1\n\t"
         "s_and_b64 exec, %[win], %[pend]\n\t"
@@ -157,7 +174,10 @@ __device__ __forceinline__ void fpp_sys_steps(uint32_t &xc, uint32_t &xm, uint32
         "v_mov_b32_dpp %[xc], %[xc] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_mov_b32_dpp %[xm], %[xm] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_mov_b32_dpp %[xu], %[xu] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
-        "s_cbranch_scc1 .LsysB%=\n"
+        "s_cbranch_scc1 .LsysB%=\n\t"
+        "s_branch .LsysEnd%=\n"
+        ".LsysMiss%=:\n\t"  // container u tested every position: a miss; stop here
+        "s_bitset0_b64 %[pend], %[u]\n"
         ".LsysEnd%=:\n\t"
         "s_mov_b64 exec, %[esv]"
         : [xc] "+v"(xc), [xm] "+v"(xm), [xu] "+v"(xu), [xl] "+v"(xl), [apos] "+v"(apos), [pend] "+s"(pend),
@@ -309,7 +329,12 @@ __device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint
                           : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap);
     uint64_t left = fpp_uniform64(so.left);
     touched = fpp_uniform64(touched);
-    if (left) fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
+    if (left) {
+        if (FP_SYS_LEFT_REFILTER)
+            fpp_refilter_loop(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk, qc, qm);
+        else
+            fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
+    }
     const uint32_t lane = __lane_id();
     const bool inq = (q >> lane) & 1ull;
     const uint64_t hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);

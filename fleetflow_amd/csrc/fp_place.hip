@@ -106,11 +106,23 @@ __global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict
     size_t head = 0;
     if (((reinterpret_cast<uintptr_t>(cpu) | reinterpret_cast<uintptr_t>(mem)) & 15u) == 0) {
         const uint4 *c4 = reinterpret_cast<const uint4 *>(cpu), *m4 = reinterpret_cast<const uint4 *>(mem);
-        for (size_t i = t; i < n / 4; i += stride) {
-            const uint4 c = c4[i], m = m4[i];
-            add(c.x, m.x); add(c.y, m.y); add(c.z, m.z); add(c.w, m.w);
+        const size_t n4 = n / 4;
+        // BM_UNROLL 16-B loads of each array in flight per thread: the 64 KB of LDS bitmaps allow
+        // two blocks per CU, too few waves to cover HBM latency one load pair at a time
+        constexpr uint32_t BM_UNROLL = 4;
+        for (size_t i0 = t; i0 < n4; i0 += BM_UNROLL * stride) {
+            uint4 c[BM_UNROLL], m[BM_UNROLL];
+#pragma unroll
+            for (uint32_t u = 0; u < BM_UNROLL; ++u) {
+                const size_t i = i0 + u * stride;
+                if (i < n4) { c[u] = c4[i]; m[u] = m4[i]; }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < BM_UNROLL; ++u) {
+                if (i0 + u * stride < n4) { add(c[u].x, m[u].x); add(c[u].y, m[u].y); add(c[u].z, m[u].z); add(c[u].w, m[u].w); }
+            }
         }
-        head = n / 4 * 4;
+        head = n4 * 4;
     }
     for (size_t i = head + t; i < n; i += stride) add(cpu[i], mem[i]);
     if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(over, 1u);

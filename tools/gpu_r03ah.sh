@@ -12,3 +12,9 @@ for v in _stats _stats_st; do
   echo "$v"; grep calls gpurun_out/${tag}_sys$v.json
 done
 bash tools/gpu_ab_lib.sh $tag "- _st -" c3,c2 || exit 1
+# value-bitmap load unroll: config-4 step and sort time, old build (_bm0) vs default
+for v in _bm0 "" _bm0 ""; do
+  FLEETPLACE_LIB=$root/fleetflow_amd/libfleetplace$v.so timeout -k 10 200 python -u bench.py --no-legs --no-stage2 --no-cpu-baseline --steps 10 \
+    > gpurun_out/${tag}_bm$v.json 2> gpurun_out/${tag}_bm$v.err || { echo "bench $v failed"; tail gpurun_out/${tag}_bm$v.err; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['breakdown_ms'])" gpurun_out/${tag}_bm$v.json "lib$v"
+done
