@@ -60,9 +60,12 @@ __device__ __forceinline__ uint32_t sys_wave_or(uint32_t x) {
 #ifndef FP_SYS_STAIR
 #define FP_SYS_STAIR 0
 #endif
-// The step loop ends at its first miss (a container that tested every live position): the group
-// is then usually full for the batch's sizes, and the containers still pending go to the serial
-// finish, whose re-test (FP_SYS_LEFT_REFILTER) drops the ones that fit no node any more.
+// A/B variants.  FP_SYS_MISS_EXIT: the step loop ends at its first miss (a container that tested
+// every live position), and the containers still pending go to the serial finish.
+// FP_SYS_LEFT_REFILTER: that finish re-tests the queue after each miss (fpp_refilter_loop).
+// Config 3 (profiles/r03ai_systolic_exit_ab.jsonl): default 64.2 / 63.9 ms, re-test finish 63.6,
+// miss exit 66.8 with the re-test and 67.5 without: a miss inside the step loop costs one lane of
+// a step, less than any serial check of it afterwards.
 #ifndef FP_SYS_MISS_EXIT
 #define FP_SYS_MISS_EXIT 0
 #endif

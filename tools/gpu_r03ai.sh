@@ -11,3 +11,4 @@ FLEETPLACE_LIB=$root/fleetflow_amd/libfleetplace_me.so timeout -k 10 400 python 
   -k "systolic or config3 or config2" -x -v --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests_me.log 2>&1 \
   || { echo "tests failed"; tail -30 gpurun_out/${tag}_tests_me.log; exit 1; }
 tail -1 gpurun_out/${tag}_tests_me.log
+bash tools/gpu_round.sh $tag tests || exit 1
