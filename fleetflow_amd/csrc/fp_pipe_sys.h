@@ -63,7 +63,8 @@ __device__ __forceinline__ uint32_t sys_wave_or(uint32_t x) {
 // A/B variants.  FP_SYS_MISS_EXIT: the step loop ends at its first miss (a container that tested
 // every live position), and the containers still pending go to the serial finish.
 // FP_SYS_LEFT_REFILTER: that finish re-tests the queue after each miss (fpp_refilter_loop).
-// Config 3 (profiles/r03ai_systolic_exit_ab.jsonl): default 64.2 / 63.9 ms, re-test finish 63.6,
+// Config 3 (profiles/r03ai_systolic_exit_ab.jsonl): default 64.2 / 63.9 ms, re-test finish 63.6
+// (alternated twice in r03ak_left_refilter_ab.jsonl: 64.1 / 63.7 vs 64.1 / 64.1, no difference),
 // miss exit 66.8 with the re-test and 67.5 without: a miss inside the step loop costs one lane of
 // a step, less than any serial check of it afterwards.
 #ifndef FP_SYS_MISS_EXIT
