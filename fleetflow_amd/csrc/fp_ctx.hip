@@ -114,7 +114,7 @@ extern "C" int fp_ctx_sync(fp_ctx *c) {
 }
 
 // the end of every fp_dev_* entry point: remember where this context's work ends
-static int dev_done(fp_ctx *c, int rc) {
+int fp_dev_done(fp_ctx *c, int rc) {
     if (hipEventRecord(c->last_ev, c->stream) != hipSuccess && rc == FP_OK) rc = FP_EDEVICE;
     return rc;
 }
@@ -220,18 +220,18 @@ extern "C" int fp_ctx_kernel_stats(fp_ctx *c, int kid, double *total_ms, uint64_
 extern "C" int fp_dev_place_batch(fp_ctx *c, const fp_batch *b) {
     if (!c || !b) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return dev_done(c, fp_dev_place_batch_impl(c, b));
+    return fp_dev_done(c, fp_dev_place_batch_impl(c, b));
 }
 extern "C" int fp_dev_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t *order,
                                uint32_t *n_cycle_dev) {
     if (!c || !g) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return dev_done(c, fp_dev_levelize_impl(c, g, level, order, n_cycle_dev));
+    return fp_dev_done(c, fp_dev_levelize_impl(c, g, level, order, n_cycle_dev));
 }
 extern "C" int fp_dev_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
     if (!c || !g) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return dev_done(c, fp_dev_legacy_order_impl(c, g, perm));
+    return fp_dev_done(c, fp_dev_legacy_order_impl(c, g, perm));
 }
 extern "C" int fp_place_ws_bytes(fp_ctx *c, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes,
                                  uint64_t *bytes_out) {
@@ -248,13 +248,13 @@ extern "C" int fp_place_geometry(fp_ctx *c, uint32_t n_scen, uint32_t n_containe
 extern "C" int fp_dev_feasibility_batch(fp_ctx *c, const fp_batch *b, uint32_t *first, uint32_t *count) {
     if (!c || !b) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return dev_done(c, fp_dev_feasibility_batch_impl(c, b, first, count));
+    return fp_dev_done(c, fp_dev_feasibility_batch_impl(c, b, first, count));
 }
 extern "C" int fp_dev_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes *ns,
                                   uint32_t *first, uint32_t *count, uint64_t *bitmap) {
     if (!c || !cs || !ns) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
-    return dev_done(c, fp_dev_feasibility_impl(c, cs, ns, first, count, bitmap));
+    return fp_dev_done(c, fp_dev_feasibility_impl(c, cs, ns, first, count, bitmap));
 }
 
 // ---- host-pointer entry points -------------------------------------------------

@@ -61,9 +61,7 @@ inline unsigned gblocks(size_t n) {
 
 }  // namespace
 
-extern "C" int fp_dev_gen_batch(fp_ctx *c, uint64_t seed, const fp_batch *b, uint32_t flags) {
-    if (!c || !b) return FP_EINVAL;
-    FP_HIP(hipSetDevice(c->device));
+static int gen_batch(fp_ctx *c, uint64_t seed, const fp_batch *b, uint32_t flags) {
     const size_t SC = (size_t)b->n_scen * b->n_containers, SN = (size_t)b->n_scen * b->n_nodes;
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_GEN, &ev);
@@ -84,4 +82,10 @@ extern "C" int fp_dev_gen_batch(fp_ctx *c, uint64_t seed, const fp_batch *b, uin
     }
     fp_prof_end(c, FP_K_GEN, ev);
     return FP_OK;
+}
+
+extern "C" int fp_dev_gen_batch(fp_ctx *c, uint64_t seed, const fp_batch *b, uint32_t flags) {
+    if (!c || !b) return FP_EINVAL;
+    FP_HIP(hipSetDevice(c->device));
+    return fp_dev_done(c, gen_batch(c, seed, b, flags));
 }

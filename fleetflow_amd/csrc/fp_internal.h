@@ -67,6 +67,9 @@ void fp_prof_end(fp_ctx *c, int kid, hipEvent_t a);
 
 // synchronise the stream, read the current kernel error word and clear it (0 or -FP_E*)
 int fp_take_err(fp_ctx *c);
+// the end of every fp_dev_* entry point (fp_ctx.hip): records c->last_ev on the context's stream,
+// which fp_ctx_set_stream waits on before a switch; returns rc (FP_EDEVICE if the record failed)
+int fp_dev_done(fp_ctx *c, int rc);
 
 // option value, or `dflt` when the option is FP_OPT_AUTO
 static inline int64_t fp_opt(const fp_ctx *c, int k, int64_t dflt) {
@@ -74,9 +77,14 @@ static inline int64_t fp_opt(const fp_ctx *c, int k, int64_t dflt) {
 }
 
 // a host-pointer call's own kernel error word for its duration (fp_internal.h fp_ctx)
+// The word is cleared on entry (stream-ordered), so an error a previous host call's kernels
+// raised after that call exited early (a HIP failure, ENOMEM mid-call) is not reported here.
 struct fp_host_err_scope {
     fp_ctx *c;
-    explicit fp_host_err_scope(fp_ctx *cc) : c(cc) { c->d_err = c->d_err_base + fp_ctx::HOST_ERR; }
+    explicit fp_host_err_scope(fp_ctx *cc) : c(cc) {
+        c->d_err = c->d_err_base + fp_ctx::HOST_ERR;
+        (void)hipMemsetAsync(c->d_err, 0, 4, c->stream);
+    }
     ~fp_host_err_scope() { c->d_err = c->d_err_base; }
 };
 

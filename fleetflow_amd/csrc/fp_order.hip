@@ -749,9 +749,14 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
                                      (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)V, 0, 32, st));
     // cnt[L] = frontier size of level L (one counter per possible level: <= V + 1)
     const size_t ncnt = (size_t)V + 2;
-    int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + (size_t)V * 8 * (1 + kShards) +
-                                   (size_t)E * 16 * kHops + kCtlWords * 4 + (size_t)CS_MAX_TILES * CS_BINS * 4 +
-                                   23 * 256);  // erec + hops, counting-sort histograms
+    // FP_OPT_LEVELIZE_SYNC = 1: the level-synchronous schedule (one launch per level); only the
+    // asynchronous one takes the vertex states, queues and edge / hop records, and only the
+    // counting sort (FP_OPT_LEVEL_SORT, on by default) its histograms
+    const bool level_sync = fp_opt(c, FP_OPT_LEVELIZE_SYNC, 0) != 0;
+    const bool counting = fp_opt(c, FP_OPT_LEVEL_SORT, 1) != 0;
+    const size_t async_ws = level_sync ? 0 : (size_t)V * 8 * (1 + kShards) + (size_t)E * 16 * kHops + kCtlWords * 4;
+    const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 : 0;
+    int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + async_ws + cs_ws + 23 * 256);
     if (rc) return rc;
     fp_ws_reset(c);
     uint32_t *indeg = (uint32_t *)fp_ws_take(c, (size_t)V * 4);
@@ -763,8 +768,9 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     uint32_t *cnt = (uint32_t *)fp_ws_take(c, ncnt * 4);
     uint32_t *ncyc = (uint32_t *)fp_ws_take(c, 64);
     void *tmp = fp_ws_take(c, sort_tmp + 16);
-    uint32_t *cs_hist = (uint32_t *)fp_ws_take(c, (size_t)CS_MAX_TILES * CS_BINS * 4);
-    if (!indeg || !fa || !fb || !keys || !keys_out || !vals || !cnt || !ncyc || !tmp || !cs_hist) return FP_ENOMEM;
+    uint32_t *cs_hist = counting ? (uint32_t *)fp_ws_take(c, cs_ws) : nullptr;
+    if (!indeg || !fa || !fb || !keys || !keys_out || !vals || !cnt || !ncyc || !tmp || (counting && !cs_hist))
+        return FP_ENOMEM;
 
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_LEVEL, &ev);
@@ -778,8 +784,6 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
             g->col, E, V, indeg, c->d_err);
         FP_HIP(hipGetLastError());
     }
-    // FP_OPT_LEVELIZE_SYNC = 1: the level-synchronous schedule (one launch per level)
-    const bool level_sync = fp_opt(c, FP_OPT_LEVELIZE_SYNC, 0) != 0;
     if (!level_sync) {
         if ((uint64_t)V + 65536ull * 64 >= 0xFFFFFFFFull) return FP_EOVERFLOW;  // queue heads stay below 2^32
         uint64_t *state = (uint64_t *)fp_ws_take(c, (size_t)V * 8);
@@ -816,7 +820,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
         k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, cyc_key, level, keys, vals, ncyc);
         FP_HIP(hipGetLastError());
-        if ((rc = level_sort(st, fp_opt(c, FP_OPT_LEVEL_SORT, 1) != 0, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
+        if ((rc = level_sort(st, counting, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
         if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
@@ -851,7 +855,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     const uint32_t cyc_key = iters + 2;
     k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, ncyc);
     FP_HIP(hipGetLastError());
-    if ((rc = level_sort(st, fp_opt(c, FP_OPT_LEVEL_SORT, 1) != 0, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
+    if ((rc = level_sort(st, counting, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
     if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
     fp_prof_end(c, FP_K_LEVEL, ev);
     return FP_OK;

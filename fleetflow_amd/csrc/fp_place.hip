@@ -850,6 +850,5 @@ extern "C" int fp_dev_argmin_cost(fp_ctx *c, const uint64_t *cost, uint32_t n, u
     if (!c || !cost || !best || n == 0) return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
     k_argmin_cost<<<1, 1024, 0, c->stream>>>(cost, n, best);
-    FP_HIP(hipGetLastError());
-    return FP_OK;
+    return fp_dev_done(c, hipGetLastError() == hipSuccess ? FP_OK : FP_EDEVICE);
 }

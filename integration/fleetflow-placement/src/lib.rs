@@ -71,6 +71,9 @@ impl Planner {
     pub fn levelize(&mut self, row_ptr: &[u32], col: &[u32], has_deps: &[u8])
                     -> Result<(Vec<u32>, Vec<u32>, u32), PlanError> {
         let v = has_deps.len();
+        if v > 0 && row_ptr.len() != v + 1 {
+            return Err(PlanError(ffi::FP_EINVAL));
+        }
         let g = ffi::fp_graph { n_vertices: v as u32, n_edges: col.len() as u32, row_ptr: row_ptr.as_ptr(),
                                 col: if col.is_empty() { std::ptr::null() } else { col.as_ptr() },
                                 has_deps: has_deps.as_ptr() };
@@ -84,6 +87,11 @@ impl Planner {
     pub fn place(&mut self, c: &Containers, nodes: &mut Nodes, level: Option<&[u32]>)
                  -> Result<(Vec<u32>, Vec<u8>), PlanError> {
         let n = c.cpu_m.len();
+        // fp_place reads every container array for n elements and reads / writes every node
+        // array for nodes.len(): a shorter Vec would be read out of bounds from safe code
+        if !c.all_len(n) || !nodes.all_len(nodes.cpu_free.len()) || level.map_or(false, |l| l.len() != n) {
+            return Err(PlanError(ffi::FP_EINVAL));
+        }
         let cs = ffi::fp_containers { n: n as u32, cpu_m: c.cpu_m.as_ptr(), mem_mib: c.mem_mib.as_ptr(),
                                       req_labels: c.req_labels.as_ptr(), conflict: c.conflict.as_ptr() };
         let mut ns = ffi::fp_nodes { n: nodes.cpu_free.len() as u32, cpu_free: nodes.cpu_free.as_mut_ptr(),
@@ -105,7 +113,8 @@ impl Planner {
     /// the updated node tables, in `b` (scenario-major arrays).
     pub fn place_batch(&mut self, b: &mut Batch) -> Result<(), PlanError> {
         let (s, c, n) = (b.n_scen as usize, b.n_containers as usize, b.n_nodes as usize);
-        let ok = b.containers.cpu_m.len() == s * c && b.nodes.cpu_free.len() == s * n
+        // every array fp_place_batch reads or writes must hold S * C (containers) or S * N (nodes)
+        let ok = b.containers.all_len(s * c) && b.nodes.all_len(s * n)
             && b.level.as_ref().map_or(true, |l| l.len() == s * c);
         if !ok {
             return Err(PlanError(ffi::FP_EINVAL));
@@ -182,6 +191,13 @@ pub struct Containers {
     pub conflict: Vec<u32>,
 }
 
+impl Containers {
+    /// every array holds exactly `n` elements
+    fn all_len(&self, n: usize) -> bool {
+        self.cpu_m.len() == n && self.mem_mib.len() == n && self.req_labels.len() == n && self.conflict.len() == n
+    }
+}
+
 /// Node table (SoA) in node-index order (`stage.servers` order, or `ORDER BY slug` for
 /// the controlplane registry, db.rs:741-750).
 pub struct Nodes {
@@ -190,6 +206,14 @@ pub struct Nodes {
     pub labels: Vec<u32>,
     pub conflict_used: Vec<u32>,
     pub schedulable: Vec<u8>,
+}
+
+impl Nodes {
+    /// every array holds exactly `n` elements
+    fn all_len(&self, n: usize) -> bool {
+        self.cpu_free.len() == n && self.mem_free.len() == n && self.labels.len() == n
+            && self.conflict_used.len() == n && self.schedulable.len() == n
+    }
 }
 
 /// `n_scen` independent what-if scenarios of `n_containers` x `n_nodes`, scenario-major
