@@ -81,3 +81,23 @@ def test_flow_plan_start_waves_end_to_end(planner, O):
     _check_waves(waves, lambda n: int(n[1:]), row_ptr, cl, level)
     script = wave_start_script(plan, "proj")
     assert len(script) == len(waves) and script[0].startswith("  wave 0: proj-live-")
+
+
+def test_config5b_full_size_placement(planner, O):
+    """BASELINE config 5b at full size: the GPU levels of the 1M-vertex DAG
+    feed the placement of its 1M containers on 100k nodes (999 CYCLE members skipped).  Assign,
+    reason and the final node state must be the oracle's, given the oracle's own levels."""
+    seed5 = SEED + 5  # bench.py SEED5
+    rp, col, hd = O.gen_dag(seed5, 1000, 500, 50, 10_000, 333)
+    level, _, ncyc = planner.levelize(rp, col, hd)
+    el, _, en = O.levelize(rp, col, hd)
+    assert ncyc == en == 999 and np.array_equal(level, el)
+    V, N = hd.size, 100_000
+    cont, nodes = O.gen_scenario(seed5, 0, V, N, 7)
+    assign, reason, after = planner.place(cont, nodes, level=level)
+    ea, er, eafter, _ = O.place(cont, nodes, level=el)
+    assert int((reason == 2).sum()) == 999
+    assert np.array_equal(assign, ea)
+    assert np.array_equal(reason, er)
+    for i in (0, 1, 3):
+        assert np.array_equal(after[i], eafter[i])
