@@ -1,0 +1,126 @@
+// Micro-benchmark: one group's exact first fit, serial exec-masked loop (fpp_group_x, fp_pipe_asm.h)
+// vs the snapshot-mask + scalar-resolve loop (fpp_res_group, fp_pipe_res.h).  Every variant must
+// produce the serial loop's assignment, records and touched set (mismatches column).
+// Patterns as tools/ubench/systolic.hip:
+//   0 fill phase (64 big nodes, identical containers)   1 mixed node types, descending memory
+//   2 config-3-like labels, ports + anti-affinity       3 partly filled group, descending demands
+//   4 full group (pass-through)
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../fleetflow_amd/csrc resolve.hip -o resolve
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "fp_pipe_asm.h"
+#include "fp_pipe_res.h"
+
+using namespace fpp;
+
+__device__ __forceinline__ uint32_t hsh(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+__device__ void setup(int pattern, uint32_t r, uint32_t lane, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
+                      uint32_t &rlab, uint32_t &cpu, uint32_t &mem, uint32_t &req, uint32_t &conf) {
+    rlab = 0; rcu = 0; req = 0; conf = 0;
+    const uint32_t ty = hsh(lane * 7 + 1 + r * 131) % 5;
+    if (pattern == 0) {
+        rcf = 64000; rmf = 262144; cpu = 4000; mem = 1024;
+    } else if (pattern == 1) {
+        rcf = 4000u << ty; rmf = ty == 4 ? 262144u : 8192u << ty;
+        rlab = ~(1u << (hsh(lane * 7 + 2) % 3));
+        cpu = 4000; mem = 16384 - lane * 64;
+        conf = hsh(lane * 7 + 3) % 10 == 0 ? 1u << (hsh(lane * 7 + 4) % 16) : 0u;
+        req = hsh(lane * 7 + 5) % 5 == 0 ? 1u << (hsh(lane * 7 + 6) % 3) : 0u;
+    } else if (pattern == 2) {
+        rcf = 4000u << ty; rmf = ty == 4 ? 262144u : 8192u << ty;
+        rlab = ~((1u << (hsh(lane * 9 + 2) % 3)) | (1u << (3 + hsh(lane * 9 + 3) % 4)) |
+                 (1u << (7 + hsh(lane * 9 + 4) % 4)) | (1u << (11 + hsh(lane * 9 + 5) % 2)));
+        cpu = 4000; mem = 16384 - lane * 64;
+        conf = (hsh(lane * 5 + 1) % 10 == 0 ? 1u << (hsh(lane * 5 + 2) % 16) : 0u) |
+               (hsh(lane * 5 + 3) % 5 == 0 ? 1u << (16 + hsh(lane * 5 + 4) % 16) : 0u);
+        req = hsh(lane * 5 + 6) % 10 < 3 ? 1u << (hsh(lane * 5 + 7) % 13) : 0u;
+    } else if (pattern == 3) {
+        rcf = hsh(lane * 11 + r) % 16000; rmf = hsh(lane * 13 + r) % 65536;
+        rlab = ~((1u << (hsh(lane * 9 + 2) % 3)) | (1u << (3 + hsh(lane * 9 + 3) % 4)));
+        cpu = 3000 - lane * 30; mem = 8192 - lane * 100;
+        conf = hsh(lane * 5 + 3 + r) % 5 == 0 ? 1u << (16 + hsh(lane * 5 + 4) % 16) : 0u;
+        req = hsh(lane * 5 + 6 + r) % 4 == 0 ? 1u << (hsh(lane * 5 + 7) % 7) : 0u;
+    } else {
+        rcf = 1000 + (hsh(lane + r) % 500); rmf = 4096; cpu = 2000 - lane; mem = 1024;
+    }
+}
+
+template <int V>
+__global__ void k_res(uint64_t *out, uint32_t *res, int pattern, uint32_t reps) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t tot = 0, nplaced = 0;
+    uint32_t asg = 0, rcf = 0, rmf = 0, rcu = 0;
+    uint64_t touched = 0;
+    for (uint32_t r = 0; r < reps; ++r) {
+        uint32_t rlab, cpu, mem, req, conf;
+        setup(pattern, r & 7, lane, rcf, rmf, rcu, rlab, cpu, mem, req, conf);
+        uint32_t qc = cpu, qm = mem;
+        for (int o = 32; o; o >>= 1) {
+            qc = min(qc, (uint32_t)__shfl_xor((int)qc, o));
+            qm = min(qm, (uint32_t)__shfl_xor((int)qm, o));
+        }
+        qc = __builtin_amdgcn_readfirstlane(qc);
+        qm = __builtin_amdgcn_readfirstlane(qm);
+        uint64_t placed = 0;
+        uint32_t nchk = 0, nhit = 0, nxt = 0;
+        touched = 0;
+        asg = 0xFFFFFFFFu;
+        const uint64_t q = ~0ull;
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        if constexpr (V == 0) {
+            fpp_group_x<0, 1>(q, placed, touched, asg, nxt, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 1u, 0u, 0u, nchk,
+                              nhit, qc, qm);
+        } else {
+            const uint64_t left = fpp_res_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm);
+            placed = q & ~left;
+        }
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+        tot += t1 - t0;
+        nplaced += __builtin_popcountll(placed);
+        if (r == reps - 1 && threadIdx.x < 64) {
+            res[lane] = asg; res[64 + lane] = rcf; res[128 + lane] = rmf; res[192 + lane] = rcu;
+            res[256 + lane] = (uint32_t)(touched >> lane) & 1u;
+        }
+    }
+    if (lane == 0) {
+        out[(threadIdx.x >> 6) * 2] = tot;
+        out[(threadIdx.x >> 6) * 2 + 1] = nplaced;
+    }
+}
+
+int main() {
+    uint64_t *d;
+    uint32_t *dr;
+    if (hipMalloc(&d, 64 * 8) != hipSuccess || hipMalloc(&dr, 5 * 64 * 4) != hipSuccess) return 1;
+    const uint32_t reps = 64;
+    const char *names[] = {"serial exec-masked (fpp_group_x)", "snapshot masks + scalar resolve"};
+    for (int pattern : {0, 1, 2, 3, 4}) {
+        uint32_t ref[320], got[320];
+        for (int v = 0; v <= 1; ++v) {
+            for (int nw : {1, 4}) {
+                uint64_t h[64] = {0};
+                for (int it = 0; it < 2; ++it) {
+                    if (hipMemset(d, 0, 64 * 8) != hipSuccess) return 1;
+                    if (v == 0) k_res<0><<<1, nw * 64>>>(d, dr, pattern, reps);
+                    else k_res<1><<<1, nw * 64>>>(d, dr, pattern, reps);
+                    if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
+                    if (hipMemcpy(h, d, 64 * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+                }
+                if (hipMemcpy(v == 0 ? ref : got, dr, sizeof(ref), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+                int bad = 0;
+                if (v) for (int i = 0; i < 320; ++i) bad += ref[i] != got[i];
+                printf("pattern %d %-34s waves %d: %7.1f cycles per container (%llu placed of %u) mismatches %d\n",
+                       pattern, names[v], nw, (double)h[0] / (64.0 * reps), (unsigned long long)h[1], 64 * reps, bad);
+            }
+        }
+    }
+    return 0;
+}
