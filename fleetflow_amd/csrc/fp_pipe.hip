@@ -32,7 +32,6 @@
 #endif
 #include "fp_pipe_asm.h"
 #include "fp_pipe_sys.h"
-#include "fp_pipe_res.h"
 #include <stdlib.h>
 #include <string.h>
 #include <type_traits>
@@ -92,8 +91,6 @@ struct PipeArgs {
     uint32_t publish; // full slots per head publish on a global link (1 when bounded: see the kernel)
     uint32_t sys;     // systolic group fill: queues of >= (sys & 0xFFFF) containers, (sys >> 16) extra
                       // steps before the serial finish (0: serial loop only)
-    uint32_t res;     // snapshot-mask + scalar-resolve group fill (fp_pipe_res.h) for queues of >= res
-                      // containers, before the systolic / serial choice (0: off)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
     uint32_t *gabort; // launch-wide abort word (bounded spins)
     uint32_t *ghead;  // [S][B-1] link control, 256 B apart: [0] head, [32] consumer tail
@@ -291,14 +288,12 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
-                                           uint32_t &nhit, uint32_t sys, uint32_t res, uint32_t &gmc, uint32_t &gmm) {
+                                           uint32_t &nhit, uint32_t sys, uint32_t &gmc, uint32_t &gmm) {
     constexpr uint32_t pf_max = G <= FP_SYS_MAX_G ? FP_PF_MAX_NARROW : FP_PF_MAX_WIDE;
     (
         [&] {
             uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
-            // the scalar resolve (narrow stages): its slot masks drop what the prefilter would
-            const bool use_res = G <= FP_SYS_MAX_G && res && (uint32_t)__builtin_popcountll(q) >= res;
-            if (pf_max > 0 && q && !use_res) {
+            if (pf_max > 0 && q) {
                 uint64_t e = __builtin_amdgcn_ballot_w64((rcf[gs] >= qc) & (rmf[gs] >= qm));
                 if (__builtin_popcountll(e) <= pf_max) {
                     bool ok = false;
@@ -324,10 +319,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                 uint64_t touched = 0;
                 // long queues (a filling group): the systolic loop, else the serial one
                 // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
-                if (use_res)
-                    fpp_group_res<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
-                                         req, conf, cand, cand_hi, gb64, nhit, qc, qm);
-                else if (G <= FP_SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
+                if (G <= FP_SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
                     fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                          req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm, sys >> 16);
                 else
@@ -872,7 +864,7 @@ k_ffd_pipe(const PipeArgs a) {
             fpp_groups<G, (G > 1), gbound>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                    used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                    (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
-                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, a.res, gmc, gmm);
+                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gmc, gmm);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
 #else
 #pragma unroll
@@ -1587,7 +1579,6 @@ struct PipeGeom {
     uint32_t resident;  // workgroups of this kernel resident on the device at once (0: unknown)
     uint32_t sys;       // systolic group fill for queues of >= sys containers (0: off)
     uint32_t sys_extra; // systolic steps past the queue length before the serial finish
-    uint32_t res;       // scalar-resolve group fill for queues of >= res containers (0: off)
 };
 
 // Global link ring size when every segment of the launch is co-resident: 256 slots x 64
@@ -1662,10 +1653,6 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
     if (g->sys_extra > 128) g->sys_extra = 128;
     if (fp_opt(c, FP_OPT_SYSTOLIC_VALU, 0) != 0) g->sys_extra |= 0x8000u;  // fp_pipe_sysv.h step loop
-    // snapshot-mask + scalar-resolve group fill (fp_pipe_res.h): queues of at least this many
-    // containers in stages of at most FP_SYS_MAX_G groups (0: off)
-    g->res = G <= FP_SYS_MAX_G ? (uint32_t)fp_opt(c, FP_OPT_RESOLVE, 0) : 0u;
-    if (g->res > 64) g->res = 64;
     return true;
 }
 
@@ -1779,7 +1766,6 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.assign = asg_s; a.reason = rsn_s; a.cost = b->cost; a.err = c->d_err;
     a.spin_ticks = (uint64_t)fp_opt(c, FP_OPT_SPIN_TICKS, (int64_t)SPIN_TICKS);
     a.sys = geo.sys ? (geo.sys | (geo.sys_extra << 16)) : 0u;
-    a.res = geo.res;
     // Head publishes on a link that holds every container (lag = S: the consumer runs a phase
     // later) are batched: FP_OPT_LINK_PUBLISH full slots per head store and vmcnt(0) drain.  A
     // bounded ring publishes every slot: its producer may wait on the consumer's tail, which
@@ -1824,7 +1810,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
 int fp_place_geometry_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t *out) {
     PipeGeom g;
     if (!pipe_geom(c, S, C, N, &g)) return FP_EOVERFLOW;
-    const uint32_t v[FP_GEOM_COUNT] = {g.G, g.W, g.B, g.R, g.lag, g.slots, g.bounded, g.resident, g.sys, g.res};
+    const uint32_t v[FP_GEOM_COUNT] = {g.G, g.W, g.B, g.R, g.lag, g.slots, g.bounded, g.resident, g.sys};
     memcpy(out, v, sizeof(v));
     return FP_OK;
 }

@@ -160,8 +160,7 @@ enum fp_option {
     FP_OPT_SYSTOLIC_VALU = 16,/* 1 = VALU-only systolic steps (fp_pipe_sysv.h), 0 = exec-masked  */
     FP_OPT_LINK_PUBLISH = 17, /* full slots per head publish on unbounded global links (auto 32) */
     FP_OPT_LEVEL_SORT = 18,   /* levelizer start order: 0 = radix sort, auto = counting sort when <= 1023 levels */
-    FP_OPT_RESOLVE = 19,      /* snapshot-mask + scalar-resolve group fill for queues of >= value containers (0 = off) */
-    FP_OPT_COUNT = 20
+    FP_OPT_COUNT = 19
 };
 int fp_ctx_set_option(fp_ctx *ctx, int option, int64_t value);
 int fp_ctx_get_option(fp_ctx *ctx, int option, int64_t *value);
@@ -198,7 +197,7 @@ int fp_place_ws_bytes(fp_ctx *ctx, uint32_t n_scen, uint32_t n_containers, uint3
  * device (options included): out[FP_GEOM_*]. */
 enum { FP_GEOM_GROUPS = 0, FP_GEOM_STAGES = 1, FP_GEOM_SEGMENTS = 2, FP_GEOM_RING = 3, FP_GEOM_LAG = 4,
        FP_GEOM_LINK_SLOTS = 5, FP_GEOM_BOUNDED = 6, FP_GEOM_RESIDENT = 7, FP_GEOM_SYSTOLIC = 8,
-       FP_GEOM_RESOLVE = 9, FP_GEOM_COUNT = 10 };
+       FP_GEOM_COUNT = 9 };
 int fp_place_geometry(fp_ctx *ctx, uint32_t n_scen, uint32_t n_containers, uint32_t n_nodes, uint32_t *out);
 int fp_dev_feasibility(fp_ctx *ctx, const fp_containers *c, const fp_nodes *nodes,
                        uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out);

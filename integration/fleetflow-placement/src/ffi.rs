@@ -40,7 +40,6 @@ pub const FP_OPT_PAYLOAD_LDS: c_int = 15;
 pub const FP_OPT_SYSTOLIC_VALU: c_int = 16;
 pub const FP_OPT_LINK_PUBLISH: c_int = 17;
 pub const FP_OPT_LEVEL_SORT: c_int = 18;
-pub const FP_OPT_RESOLVE: c_int = 19;
 pub const FP_GEOM_GROUPS: usize = 0;
 pub const FP_GEOM_STAGES: usize = 1;
 pub const FP_GEOM_SEGMENTS: usize = 2;
@@ -50,8 +49,7 @@ pub const FP_GEOM_LINK_SLOTS: usize = 5;
 pub const FP_GEOM_BOUNDED: usize = 6;
 pub const FP_GEOM_RESIDENT: usize = 7;
 pub const FP_GEOM_SYSTOLIC: usize = 8;
-pub const FP_GEOM_RESOLVE: usize = 9;
-pub const FP_GEOM_COUNT: usize = 10;
+pub const FP_GEOM_COUNT: usize = 9;
 
 /// Opaque `fp_ctx` (one per host thread; owns a HIP stream on one MI355X).
 #[repr(C)]

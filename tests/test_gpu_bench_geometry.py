@@ -200,64 +200,3 @@ def test_screen_vs_unscreened_and_oracle(S, C, N, planner, O, opts):
         assert int(c1[s]) == O.cost(ea, N, base + s)
         for i in (0, 1, 3):
             assert np.array_equal(n1[i][s * N:(s + 1) * N], eafter[i])
-
-
-# ---- snapshot-mask + scalar-resolve group fill (fp_pipe_res.h) ------------------------------------
-@pytest.mark.parametrize("thr", [1, 24])
-@pytest.mark.parametrize("C,N,flags,w,seg", [(20_000, 6_000, 7, 4, 4), (60_000, 12_000, 7, 4, 4),
-                                             (4_000, 641, 7, 1, 12), (30_000, 2_000, 7, 4, 40), (64, 64, 7, 4, 4),
-                                             (40_000, 3_000, 7, 2, 2), (9_000, 700, 5, 1, 1),
-                                             (50_000, 3_000, 3, 4, 4)])
-def test_resolve_fill_vs_oracle(C, N, flags, w, seg, thr, planner, O, opts):
-    """Group queues of >= thr containers take the scalar resolve (thr 1: every queue), the rest the
-    systolic / serial loops; plan, reasons and final node state must be the oracle's.  Compiled
-    for stages of at most 4 groups: wider stages report 0 and run the other loops."""
-    opts(resolve=thr, pipe_w=w, pipe_seg=seg)
-    g = planner.geometry(1, C, N)
-    assert g["resolve"] == (thr if g["groups"] <= 4 else 0), g
-    cont, nodes = O.gen_scenario(SEED4 + 29 * C + N, 3, C, N, flags)
-    assign, reason, after = planner.place(cont, nodes)
-    ea, er, eafter, _ = O.place(cont, nodes)
-    assert np.array_equal(assign, ea)
-    assert np.array_equal(reason, er)
-    for i in (0, 1, 3):
-        assert np.array_equal(after[i], eafter[i])
-
-
-@pytest.mark.parametrize("thr", [1, 16])
-def test_resolve_zero_labels_cycles_cordons(thr, planner, O, opts):
-    """The resolve on a many-scenario batch with all-zero containers, label-only containers (cpu =
-    mem = conflict = 0, req != 0: they change no record), cycles, cordoned nodes and more than 32
-    live nodes per group (chunks)."""
-    opts(resolve=thr)
-    S, C, N, base = 6, 5_000, 3_000, 91
-    rng = np.random.default_rng(100 + thr)
-    conts, nodes, levels = [], [], []
-    for s in range(S):
-        c, n = O.gen_scenario(SEED4 + 37, base + s, C, N, 7)
-        c = [np.array(a, np.uint32) for a in c]
-        z = rng.random(C) < 0.03
-        for a in c:
-            a[z] = 0
-        lo = rng.random(C) < 0.03                      # label-only containers
-        c[0][lo] = 0
-        c[1][lo] = 0
-        c[3][lo] = 0
-        c[2][lo] = np.uint32(1) << rng.integers(0, 13, int(lo.sum())).astype(np.uint32)
-        n = [np.array(a) for a in n]
-        n[4] = n[4].astype(np.uint8)
-        n[4][rng.random(N) < 0.1] = 0
-        conts.append(c)
-        nodes.append(n)
-        levels.append(np.where(rng.random(C) < 0.01, 0xFFFFFFFF, 0).astype(np.uint32))
-    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
-    assign, reason, cost, after = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
-                                                      [cat(nodes, i) for i in range(5)],
-                                                      level=np.concatenate(levels), scen_base=base)
-    for s in range(S):
-        ea, er, eafter, _ = O.place(conts[s], nodes[s], level=levels[s])
-        assert np.array_equal(assign[s * C:(s + 1) * C], ea), s
-        assert np.array_equal(reason[s * C:(s + 1) * C], er), s
-        assert int(cost[s]) == O.cost(ea, N, base + s)
-        for i in (0, 1, 3):
-            assert np.array_equal(after[i][s * N:(s + 1) * N], eafter[i])

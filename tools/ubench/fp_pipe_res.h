@@ -94,6 +94,9 @@ __device__ __forceinline__ void fpp_res_chain(uint64_t q, uint32_t vm, uint32_t 
 // One group's queue q.  Records rcf/rmf/rcu/rlab (lane = node; rlab = ~labels), containers
 // cpu/mem/req/conf (lane = queue position), batch corner (qc, qm).  Placed containers get
 // asg = gbg | node lane; touched |= nodes placed on.  Returns the queued lanes left unplaced.
+// PERM: the table is compacted by one ds_permute per record (live lane l pushes to lane slot(l)),
+// else by K v_writelane per record (microbenchmark A/B).
+template <bool PERM = true>
 __device__ __forceinline__ uint64_t fpp_res_group(uint64_t q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
                                                   uint32_t &rmf, uint32_t &rcu, uint32_t rlab, uint32_t cpu,
                                                   uint32_t mem, uint32_t req, uint32_t conf, uint32_t gbg,
@@ -105,45 +108,59 @@ __device__ __forceinline__ uint64_t fpp_res_group(uint64_t q, uint64_t &touched,
         uint64_t ch = live;
         if (__builtin_popcountll(ch) > FP_RES_MAX) {
             uint64_t e = ch;
+#pragma unroll 1
             for (int i = 0; i < FP_RES_MAX; ++i) e &= e - 1;
             ch &= ~e;
         }
         live &= ~ch;
         const uint32_t K = (uint32_t)__builtin_popcountll(ch);
-        // table + slot masks, node-major from the highest slot down (bit k = slot k)
-        uint32_t tcf = 0, tmf = 0, tcu = lane == 63 ? 0xFFFFFFFFu : 0u, vm = 0;  // lane 63: the sentinel
-        uint64_t e = ch;
-        for (uint32_t k = K; k-- > 0;) {
-            const uint32_t l = 63u - (uint32_t)__builtin_clzll(e);
-            e &= ~(1ull << l);
-            const uint32_t cf = __builtin_amdgcn_readlane(rcf, l), mf = __builtin_amdgcn_readlane(rmf, l);
-            const uint32_t cu = __builtin_amdgcn_readlane(rcu, l), nl = __builtin_amdgcn_readlane(rlab, l);
-            const bool fit = (cpu <= cf) & (mem <= mf) & (((req & nl) | (conf & cu)) == 0u);
-            vm = (vm << 1) | (fit ? 1u : 0u);
-            tcf = (uint32_t)fp_res_writelane((int)cf, (int)k, (int)tcf);
-            tmf = (uint32_t)fp_res_writelane((int)mf, (int)k, (int)tmf);
-            tcu = (uint32_t)fp_res_writelane((int)cu, (int)k, (int)tcu);
+        // slot of a live lane = live lanes below it
+        const uint32_t my = __builtin_amdgcn_mbcnt_hi((uint32_t)(ch >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ch, 0u));
+        const bool in = (ch >> lane) & 1ull;
+        uint32_t tcf, tmf, tcu, tln, vm = 0;
+        if (PERM) {
+            // live lane l -> lane slot(l); the others park on lane 62 (K <= 32: never a slot)
+            const int dst = (int)((in ? my : 62u) << 2);
+            tcf = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)rcf);
+            tmf = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)rmf);
+            tcu = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)rcu);
+            const uint32_t tnl = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)rlab);
+            tln = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)lane);
+            // slot masks, node-major from the highest slot down (bit k = slot k)
+#pragma unroll 1
+            for (uint32_t k = K; k-- > 0;) {
+                const uint32_t cf = __builtin_amdgcn_readlane(tcf, k), mf = __builtin_amdgcn_readlane(tmf, k);
+                const uint32_t cu = __builtin_amdgcn_readlane(tcu, k), nl = __builtin_amdgcn_readlane(tnl, k);
+                const bool fit = (cpu <= cf) & (mem <= mf) & (((req & nl) | (conf & cu)) == 0u);
+                vm = (vm << 1) | (fit ? 1u : 0u);
+            }
+        } else {
+            tcf = 0; tmf = 0; tcu = 0; tln = 0;
+            uint64_t e = ch;
+            for (uint32_t k = K; k-- > 0;) {
+                const uint32_t l = 63u - (uint32_t)__builtin_clzll(e);
+                e &= ~(1ull << l);
+                const uint32_t cf = __builtin_amdgcn_readlane(rcf, l), mf = __builtin_amdgcn_readlane(rmf, l);
+                const uint32_t cu = __builtin_amdgcn_readlane(rcu, l), nl = __builtin_amdgcn_readlane(rlab, l);
+                const bool fit = (cpu <= cf) & (mem <= mf) & (((req & nl) | (conf & cu)) == 0u);
+                vm = (vm << 1) | (fit ? 1u : 0u);
+                tcf = (uint32_t)fp_res_writelane((int)cf, (int)k, (int)tcf);
+                tmf = (uint32_t)fp_res_writelane((int)mf, (int)k, (int)tmf);
+                tcu = (uint32_t)fp_res_writelane((int)cu, (int)k, (int)tcu);
+                tln = (uint32_t)fp_res_writelane((int)l, (int)k, (int)tln);
+            }
         }
+        // lane 63: the sentinel (fpp_res_chain)
+        if (lane == 63) { tcf = 0u; tmf = 0u; tcu = 0xFFFFFFFFu; }
         uint32_t slot = 0xFFFFFFFFu;
         fpp_res_chain(q, vm, cpu, mem, conf, tcf, tmf, tcu, slot);
         // write the chunk's records back: live lane l holds slot popcount(ch below l)
-        const uint32_t my = __builtin_amdgcn_mbcnt_hi((uint32_t)(ch >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ch, 0u));
-        const bool in = (ch >> lane) & 1ull;
         const uint32_t ncf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(my << 2), (int)tcf);
         const uint32_t nmf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(my << 2), (int)tmf);
         const uint32_t ncu = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(my << 2), (int)tcu);
         touched |= __builtin_amdgcn_ballot_w64(in && (ncf != rcf || nmf != rmf || ncu != rcu));
         if (in) { rcf = ncf; rmf = nmf; rcu = ncu; }
-        // placed containers: slot -> node lane (the slot-th set bit of ch), through a lane table
-        uint32_t tln = 0;
-        {
-            uint64_t f = ch;
-            for (uint32_t k = 0; k < K; ++k) {
-                const uint32_t l = (uint32_t)__builtin_ctzll(f);
-                f &= f - 1;
-                tln = (uint32_t)fp_res_writelane((int)l, (int)k, (int)tln);
-            }
-        }
+        // placed containers: slot -> node lane
         const bool hit = ((q >> lane) & 1ull) && slot != 0xFFFFFFFFu;
         const uint32_t nl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((slot & 63u) << 2), (int)tln);
         if (hit) asg = gbg | nl;
@@ -160,8 +177,8 @@ __device__ __forceinline__ void fpp_group_res(uint64_t q, uint64_t &placed, uint
                                               uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
                                               uint32_t cand, uint32_t cand_hi, uint32_t gb64, uint32_t &nhit,
                                               uint32_t qc, uint32_t qm) {
-    const uint64_t left = fpp_res_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u,
-                                        qc, qm);
+    const uint64_t left = fpp_res_group<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf,
+                                              gb64 + g * 64u, qc, qm);
     const uint64_t hit = q & ~left;
 #ifdef FP_PIPE_STATS
     nhit += (uint32_t)__builtin_popcountll(hit);

@@ -5,13 +5,13 @@
 //   0 fill phase (64 big nodes, identical containers)   1 mixed node types, descending memory
 //   2 config-3-like labels, ports + anti-affinity       3 partly filled group, descending demands
 //   4 full group (pass-through)
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../fleetflow_amd/csrc resolve.hip -o resolve
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I. -I../../fleetflow_amd/csrc resolve.hip -o resolve
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 
 #include "fp_pipe_asm.h"
-#include "fp_pipe_res.h"
+#include "fp_pipe_res.h"  // tools/ubench (the experiment lives here)
 
 using namespace fpp;
 
@@ -78,7 +78,8 @@ __global__ void k_res(uint64_t *out, uint32_t *res, int pattern, uint32_t reps) 
             fpp_group_x<0, 1>(q, placed, touched, asg, nxt, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 1u, 0u, 0u, nchk,
                               nhit, qc, qm);
         } else {
-            const uint64_t left = fpp_res_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm);
+            const uint64_t left = V == 1 ? fpp_res_group<false>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm)
+                                         : fpp_res_group<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm);
             placed = q & ~left;
         }
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -101,16 +102,17 @@ int main() {
     uint32_t *dr;
     if (hipMalloc(&d, 64 * 8) != hipSuccess || hipMalloc(&dr, 5 * 64 * 4) != hipSuccess) return 1;
     const uint32_t reps = 64;
-    const char *names[] = {"serial exec-masked (fpp_group_x)", "snapshot masks + scalar resolve"};
+    const char *names[] = {"serial exec-masked (fpp_group_x)", "resolve, writelane table", "resolve, ds_permute table"};
     for (int pattern : {0, 1, 2, 3, 4}) {
         uint32_t ref[320], got[320];
-        for (int v = 0; v <= 1; ++v) {
+        for (int v = 0; v <= 2; ++v) {
             for (int nw : {1, 4}) {
                 uint64_t h[64] = {0};
                 for (int it = 0; it < 2; ++it) {
                     if (hipMemset(d, 0, 64 * 8) != hipSuccess) return 1;
                     if (v == 0) k_res<0><<<1, nw * 64>>>(d, dr, pattern, reps);
-                    else k_res<1><<<1, nw * 64>>>(d, dr, pattern, reps);
+                    else if (v == 1) k_res<1><<<1, nw * 64>>>(d, dr, pattern, reps);
+                    else k_res<2><<<1, nw * 64>>>(d, dr, pattern, reps);
                     if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
                     if (hipMemcpy(h, d, 64 * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
                 }
