@@ -24,12 +24,8 @@
 // candidate groups get the exact check.
 #include "fp_internal.h"
 // The candidate loop is group-major (below): every register access uses a compile-time
-// group index.  -DFP_LEGACY_LOOP builds round 1's container-major loops instead (the
-// hand-scheduled fp_pipe_asm.h loop for 2..10-group stages, C++ elsewhere; add
-// -DFP_NO_ASM for C++ everywhere) -- kept for A/B measurements.
-#if defined(FP_LEGACY_LOOP) && !defined(FP_NO_ASM)
-#define FP_ASM
-#endif
+// group index.  (Round 1's container-major loops and the A/B variants of rounds 2-3 are in git
+// history; DESIGN.md 7 keeps their numbers.)
 #include "fp_pipe_asm.h"
 #include "fp_pipe_sys.h"
 #include <stdlib.h>
@@ -73,9 +69,7 @@ constexpr uint32_t CYC = 0x80000000u;
 // launch, so the bound is wall-clock time, not an iteration count.
 constexpr uint64_t SPIN_TICKS = 100ull * 1000 * 1000 * 60;  // 60 s (FP_OPT_SPIN_TICKS overrides: tests)
 constexpr uint32_t MAX_G = 16;      // groups per stage (4 record VGPRs per group)
-#ifndef FP_SPIN_MAX
-#define FP_SPIN_MAX 12              // longest back-off sleep of an idle stage (x 64 cycles)
-#endif
+constexpr int SPIN_MAX = 12;         // longest back-off sleep of an idle stage (x 64 cycles)
 constexpr int NF = 5;               // ring fields: cpu, mem, req, conf, idx
 constexpr uint32_t IDX_POS_MASK = (1u << 21) - 1;  // position bits of a packed s_idx word
 
@@ -151,13 +145,10 @@ __device__ __forceinline__ bool spin(uint32_t *word, Pred pred, uint32_t *abort_
         // back off: a spinning wave still takes issue slots from its CU's busy waves
         if (n < 8) __builtin_amdgcn_s_sleep(1);
         else if (n < 32) __builtin_amdgcn_s_sleep(4);
-        else __builtin_amdgcn_s_sleep(FP_SPIN_MAX);
+        else __builtin_amdgcn_s_sleep(SPIN_MAX);
     }
 }
 
-// lane `t` of `old` replaced by the wave-uniform `val` (v_cmp + v_cndmask)
-// v_writelane_b32 (no clang builtin for it in this toolchain; the LLVM intrinsic by name)
-extern "C" __device__ int fp_writelane(int val, int lane_sel, int old) __asm("llvm.amdgcn.writelane.i32");
 
 // bucket index: largest k with T[k] <= v (T ascending, T[0] = 0; lane base + k holds
 // T[k]).  Binary search through ds_bpermute: no scalar registers held across the
@@ -184,15 +175,6 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
-}
 
 constexpr size_t LCTL = 64;  // u32 per global link control block: [0] head, [LCTL / 2] tail
 
@@ -221,7 +203,7 @@ __device__ __forceinline__ bool gring_wait(uint32_t *tail, uint32_t need, uint32
             }
         }
         if (n < 8) __builtin_amdgcn_s_sleep(2);
-        else __builtin_amdgcn_s_sleep(FP_SPIN_MAX);
+        else __builtin_amdgcn_s_sleep(SPIN_MAX);
     }
 }
 
@@ -236,14 +218,9 @@ __device__ __forceinline__ bool gring_wait(uint32_t *tail, uint32_t need, uint32
 //                               CNT [0]=n_used [1]=n_rej [2]=abort
 //   D   : (W-1)*R*NF*64 u32     ring slots, field-major
 // a tile's records of one kind, one register per group (a plain array, register-promoted
-// with static indices; a pinned tuple in the legacy asm build)
-#ifdef FP_ASM
-template <uint32_t G>
-using RecT = typename std::conditional<(G >= 2 && G <= 10), rec10, uint32_t[G]>::type;
-#else
+// with static indices)
 template <uint32_t G>
 using RecT = uint32_t[G];
-#endif
 
 // the group-major loop over a stage's groups, g a compile-time constant in every call.
 // After a group's queue: the used-node bits and (UPD) the bucket masks catch up with the
@@ -256,40 +233,24 @@ using RecT = uint32_t[G];
 // next candidate group without a serial check.  The test is vector-parallel over the
 // queue: the nodes that could take the batch's smallest demands (the batch corner, qc/qm)
 // are broadcast one at a time and every lane tests its own container.  It pays while the
-// corner holds few nodes (the filled-up frontier group); above FP_PF_MAX nodes the queue
+// corner holds few nodes (the filled-up frontier group); above PF_MAX_* nodes the queue
 // goes to the serial loop unfiltered.
-// Corner-node limit of the prefilter, by stage width (tools/gpu_ab_lib.sh, r03m_ab*.jsonl):
-// narrow (<= 4-group) stages 4 -- config 3 65.3 -> 64.1 ms (16: 65.3, 32: 70.8); wide stages
-// off -- config 4 17.54 -> 17.28 ms (4: 17.48, 32: 17.96).  FP_PF_MAX overrides both.
-#ifdef FP_PF_MAX
-#define FP_PF_MAX_NARROW FP_PF_MAX
-#define FP_PF_MAX_WIDE FP_PF_MAX
-#endif
-#ifndef FP_PF_MAX_NARROW
-#define FP_PF_MAX_NARROW 4
-#endif
-#ifndef FP_PF_MAX_WIDE
-#define FP_PF_MAX_WIDE 0
-#endif
-// systolic group fill (fp_pipe_sys.h) in stages of at most this many groups
-#ifndef FP_SYS_MAX_G
-#define FP_SYS_MAX_G 4
-#endif
-// the serial loop over one group's queue: the exec-masked loop (fp_pipe_asm.h,
-// fpp_group_x: 172 vs 264 cycles per container in tools/ubench/place.hip); -DFP_GROUP_LOOP=
-// fpp_asm_group selects round 2's readlane / writelane loop for A/B runs
-#ifndef FP_GROUP_LOOP
-#define FP_GROUP_LOOP fpp_group_x
-#endif
-#define FPP_GROUP_LOOP FP_GROUP_LOOP
-template <uint32_t G, bool UPD, bool GB, uint32_t... gs, class Rec>
+// Corner-node limit of the prefilter, by stage width (r03m A/B, profiles/r03m_ab*.jsonl): narrow
+// (<= 4-group) stages 4 -- config 3 65.3 -> 64.1 ms (16: 65.3, 32: 70.8); wide stages off -- config
+// 4 17.54 -> 17.28 ms (4: 17.48, 32: 17.96).
+constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
+// the systolic group fill (fp_pipe_sys.h) is compiled for stages of at most this many groups
+constexpr uint32_t SYS_MAX_G = 4;
+// The serial loop over one group's queue is the exec-masked loop (fp_pipe_asm.h fpp_group_x:
+// 172 vs 264 cycles per container for round 2's readlane / writelane loop).
+template <uint32_t G, bool UPD, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
-                                           uint32_t &nhit, uint32_t sys, uint32_t &gmc, uint32_t &gmm) {
-    constexpr uint32_t pf_max = G <= FP_SYS_MAX_G ? FP_PF_MAX_NARROW : FP_PF_MAX_WIDE;
+                                           uint32_t &nhit, uint32_t sys) {
+    constexpr uint32_t pf_max = G <= SYS_MAX_G ? PF_MAX_NARROW : PF_MAX_WIDE;
     (
         [&] {
             uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
@@ -319,18 +280,13 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                 uint64_t touched = 0;
                 // long queues (a filling group): the systolic loop, else the serial one
                 // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
-                if (G <= FP_SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
+                if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
                     fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                          req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm, sys >> 16);
                 else
-                    FPP_GROUP_LOOP<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
-                                         req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
+                    fpp_group_x<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                                       req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
                 if (touched) {
-                    if (GB) {  // the group's bounds (largest free cpu / mem) after its placements
-                        const uint32_t xc = wave_max(rcf[gs]), xm = wave_max(rmf[gs]);
-                        gmc = lane == gs ? xc : gmc;
-                        gmm = lane == gs ? xm : gmm;
-                    }
                     const bool me = (touched >> lane) & 1ull;
                     if (gs < 32) used |= me ? (1u << gs) : 0u;
                     else used_hi |= me ? (1u << (gs & 31)) : 0u;
@@ -356,50 +312,23 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
         ...);
 }
 
-// BLK: 1024 for multi-stage segments (W <= 16 waves, <= 128 VGPRs each); 64 for the
-// one-wave segments of the wide geometry, whose 13..40 groups of records take 4 VGPRs per
-// group.  FP_WIDE_WAVES = the waves per SIMD the one-wave kernels are compiled for (3: at
-// most 168 VGPRs, 12 segments in flight per CU)
-#ifndef FP_WIDE_WAVES
-#define FP_WIDE_WAVES 3
-#endif
-// One-wave segments of 12 groups (many-scenario batches) are compiled as 64-thread kernels for
-// FP_WIDE12_WAVES waves per SIMD: 5 fits them in 96 VGPRs (32 B of scratch) and 20 segments per
-// CU -- config-4 FFD 20.9 -> 18.7 ms against the 1024-thread kernel's 107 VGPRs and four waves
-// (6 waves: 80 VGPRs, 100 B of scratch, 19.2 ms).  0 selects the 1024-thread kernel.
-// Batch prescan: skip a group's bucket-mask loads when its corner is empty, in the wide stages
-// (config-4 FFD 17.38 -> 15.72 ms; a batch that passes a segment mostly has every corner empty).
-// The narrow stages keep the branch-free form (config 3: 64.3 vs 65.3 ms with the skip).
-// (r03z A/B, profiles/r03z_prescan_ab.jsonl)
-#ifndef FP_PRESCAN_SKIP_WIDE
-#define FP_PRESCAN_SKIP_WIDE 1
-#endif
-#ifndef FP_PRESCAN_SKIP_NARROW
-#define FP_PRESCAN_SKIP_NARROW 0
-#endif
-// A/B variant: per-group bounds of the largest free cpu / mem skip the corner ballots.  Slower
-// (config-4 FFD 15.73 vs 15.08 ms, profiles/r03af_bound_ab.jsonl): the bounds' upkeep after a
-// group's placements costs more than the ballots they save.
-#ifndef FP_GROUP_BOUND
-#define FP_GROUP_BOUND 0
-#endif
-// skip the group loop when no container of the batch has a candidate group (config-4 FFD
-// 15.62 -> 15.06 ms, config 3 64.3 -> 63.6 ms;
-// profiles/r03aa_todo_ab.jsonl, r03ab_todo_ab.jsonl)
-// A/B variant: req / conf of link input loaded after the prescan, only for batches with a
-// candidate.  Slower (config-4 FFD 15.45 vs 15.08 ms, profiles/r03ac_defer_ab.jsonl): the kernel
-// is issue-bound, and a batch with a candidate then waits on a second load round trip.
-#ifndef FP_DEFER_RC
-#define FP_DEFER_RC 0
-#endif
-#ifndef FP_TODO_SKIP
-#define FP_TODO_SKIP 1
-#endif
-#ifndef FP_WIDE12_WAVES
-#define FP_WIDE12_WAVES 5
-#endif
+// BLK: 1024 for multi-stage segments (W <= 16 waves, <= 128 VGPRs each); 64 for the one-wave
+// segments of the wide geometry, whose 13..40 groups of records take 4 VGPRs per group, compiled
+// for WIDE_WAVES waves per SIMD (3: at most 168 VGPRs, 12 segments in flight per CU).
+// One-wave segments of 12 groups (many-scenario batches) are compiled for WIDE12_WAVES waves per
+// SIMD: 5 fits them in 96 VGPRs (32 B of scratch) and 20 segments per CU -- config-4 FFD 20.9 ->
+// 18.7 ms against the 1024-thread kernel's 107 VGPRs and four waves (6 waves: 80 VGPRs, 100 B of
+// scratch, 19.2 ms).
+constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
+// Batch prescan: a group with an empty batch corner skips its bucket-mask loads in the wide stages
+// (config-4 FFD 17.38 -> 15.72 ms: a batch that passes a segment mostly has every corner empty);
+// the narrow stages keep the branch-free form (config 3: 64.3 vs 65.3 ms with the skip; r03z A/B,
+// profiles/r03z_prescan_ab.jsonl).  A batch without candidates skips the group loop (config-4
+// FFD 15.62 -> 15.06 ms, config 3 64.3 -> 63.6 ms; r03aa/r03ab).  Measured slower and removed in
+// round 4: per-group capacity bounds in place of the corner ballots (15.73 vs 15.08
+// ms, r03af), req / conf of link input loaded after the prescan (15.45 vs 15.08 ms, r03ac).
 template <uint32_t G, uint32_t BLK>
-__global__ __launch_bounds__(BLK, BLK == 64 ? (G == 12 && FP_WIDE12_WAVES ? FP_WIDE12_WAVES : FP_WIDE_WAVES) : 1) void
+__global__ __launch_bounds__(BLK, BLK == 64 ? (G == 12 ? WIDE12_WAVES : WIDE_WAVES) : 1) void
 k_ffd_pipe(const PipeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = a.W, R = a.R, B = a.B;
@@ -489,19 +418,6 @@ k_ffd_pipe(const PipeArgs a) {
             zs_l = (uint32_t)__builtin_ctzll(sm);
         }
     }
-    // group bounds (wide stages, FP_GROUP_BOUND): lane g holds an upper bound of group g's largest
-    // free cpu / mem.  Free capacity only shrinks, so a stale bound stays an upper bound; groups
-    // whose bounds are below the batch corner skip the exact corner ballot.
-    constexpr bool gbound = FP_GROUP_BOUND && G > FP_SYS_MAX_G && G <= 64;
-    uint32_t gmc = 0, gmm = 0;
-    if (gbound) {
-#pragma unroll
-        for (uint32_t g = 0; g < G; ++g) {
-            const uint32_t xc = wave_max(rcf[g]), xm = wave_max(rmf[g]);
-            gmc = lane == g ? xc : gmc;
-            gmm = lane == g ? xm : gmm;
-        }
-    }
     // bucket-major (a rolled loop): two thresholds live in scalars at a time -- hoisting all
     // 64 of them out of an unrolled loop spilled scalars into VGPR lanes
 #pragma unroll 1
@@ -521,9 +437,6 @@ k_ffd_pipe(const PipeArgs a) {
     __syncthreads();
 
     const bool has_out = w + 1 < W;
-    // a global-link consumer that forwards positions only (the segment's last stage) loads a
-    // container's req / conf after the prescan, when the batch has a candidate here
-    const bool defer_rc = FP_DEFER_RC && !has_out;
     const bool g_in = w == 0 && b > 0;                  // input from segment b-1
     const bool g_out = w + 1 == W && b + 1 < B;         // output to segment b+1
     // a global link slot: [0] = count (or END), [64..127] = the containers' FFD positions;
@@ -552,10 +465,6 @@ k_ffd_pipe(const PipeArgs a) {
     uint32_t opend = 0;
     uint32_t n_used = 0, n_rej = 0;
     uint32_t st_spin_in = 0, st_spin_out = 0, st_visits = 0, st_checks = 0, st_hits = 0, st_batches = 0;
-    // diagnostics (C++ loop, stats build): why candidate checks miss -- [0] cpu and mem fit some
-    // node (a label or conflict test failed), [1] cpu+mem+labels fit (conflict failed), [2] cpu
-    // fits some node but mem none, [3] mem fits some node but cpu none
-    uint32_t st_miss[4] = {0, 0, 0, 0};
     unsigned long long ck_in = 0, ck_pre = 0, ck_cand = 0, ck_fwd = 0, ck_wait = 0;
     const unsigned long long ck_t0 = STAT_CLK();
     unsigned long long ck_a, ck_b;
@@ -589,7 +498,7 @@ k_ffd_pipe(const PipeArgs a) {
                     }
                 }
                 if (n_sp < 8) __builtin_amdgcn_s_sleep(2);
-                else __builtin_amdgcn_s_sleep(FP_SPIN_MAX);
+                else __builtin_amdgcn_s_sleep(SPIN_MAX);
             }
             st_spin_in += n_sp;
             if (!got) break;
@@ -610,10 +519,8 @@ k_ffd_pipe(const PipeArgs a) {
                 const uint32_t p = pos & pmask;
                 cpu = a.s_cpu[cb + p];
                 mem = a.s_mem[cb + p];
-                if (!defer_rc) {
-                    req = a.s_req[cb + p];
-                    conf = a.s_conf[cb + p];
-                }
+                req = a.s_req[cb + p];
+                conf = a.s_conf[cb + p];
             }
             itail++;
         } else if (w == 0) {
@@ -694,12 +601,10 @@ k_ffd_pipe(const PipeArgs a) {
         const uint32_t qm = wave_min(valid ? mem : 0xFFFFFFFFu);
         // every mask load is issued before the first use (no per-group LDS round trip)
         const uint32_t oc = kc * 2, om = km * 2 + 1;
-        constexpr bool prescan_skip = G > FP_SYS_MAX_G ? FP_PRESCAN_SKIP_WIDE : FP_PRESCAN_SKIP_NARROW;
+        constexpr bool prescan_skip = G > SYS_MAX_G;
         GM cand = 0;
-        const uint64_t galive = gbound ? __builtin_amdgcn_ballot_w64((gmc >= qc) & (gmm >= qm)) : ~0ull;
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
-            if (gbound && !((galive >> g) & 1ull)) continue;  // no node of g reaches the corner
             const uint64_t e = __builtin_amdgcn_ballot_w64((rcf[g] >= qc) & (rmf[g] >= qm));
             const uint64_t *mg = Mw + (size_t)g * K * 2;
             if (prescan_skip) {
@@ -711,14 +616,6 @@ k_ffd_pipe(const PipeArgs a) {
             }
         }
         cand = valid ? cand : GM(0);
-        if (defer_rc && g_in && (__builtin_amdgcn_ballot_w64(cand != 0) != 0 || (qc | qm) == 0u)) {
-            // labels and conflicts, needed only when some container has a candidate group (or a
-            // zero demand: then qc = qm = 0).  A batch that passes the segment forwards positions.
-            if (valid) {
-                req = a.s_req[cb + (idx & pmask)];
-                conf = a.s_conf[cb + (idx & pmask)];
-            }
-        }
         const bool zero = valid && (cpu | mem | req | conf) == 0u;
         uint64_t todo = __builtin_amdgcn_ballot_w64(cand != 0 && !zero);
         uint64_t placed = 0;
@@ -732,115 +629,6 @@ k_ffd_pipe(const PipeArgs a) {
         const unsigned long long tl_pre = ck_b;
         const uint32_t tl_checks0 = st_checks, tl_hits0 = st_hits, tl_todo = (uint32_t)__popcll(todo);
 #endif
-#ifdef FP_LEGACY_LOOP
-#  ifdef FP_ASM
-        // Exact first fit, container by container in FFD order: the hand-scheduled
-        // loop (fp_pipe_asm.h) for 2..10-group stages.  Same algorithm as the C++ loop below.
-        if constexpr (G >= 2 && G <= 10) {
-            const uint32_t lane_sel = lane < 32u ? 0xFFFFFFFFu : 0u;
-            const uint32_t maddr = (uint32_t)(size_t)(__attribute__((address_space(3))) uint64_t *)(
-                Mw + (lane & (K - 1)) * 2 + (lane >> 5));
-            uint32_t nchk = 0, nhit = 0;
-            fpp_asm_batch(todo, placed, my_assign, usedbits, rcf, rmf, rcu, rlab, cpu, mem, req, conf, cand, my_t,
-                          lane_sel, maddr, (gbase * 64u), nchk, nhit);
-            if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
-        } else
-#  endif
-        if constexpr (G == 1) {
-            // one-group stages (few scenarios): every todo container has exactly one
-            // candidate group, so one check each and no candidate bookkeeping
-            while (todo) {
-                const uint32_t ti = (uint32_t)__builtin_ctzll(todo);
-                todo &= todo - 1;
-                const uint32_t c_cpu = __builtin_amdgcn_readlane(cpu, ti);
-                const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
-                const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
-                const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
-                const uint32_t x = rcf[0], y = rmf[0], z = rcu[0];
-                if (STAT_ON) st_checks++;
-                const uint64_t m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
-                                   __builtin_amdgcn_ballot_w64(((rlab[0] & c_req) | (z & c_conf)) == 0u);
-                if (m) {
-                    const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                    const uint32_t oc = __builtin_amdgcn_readlane(x, l);
-                    const uint32_t om = __builtin_amdgcn_readlane(y, l);
-                    const uint32_t nc = oc - c_cpu, nm = om - c_mem;
-                    const bool me = lane == l;
-                    rcf[0] = me ? nc : x;
-                    rmf[0] = me ? nm : y;
-                    rcu[0] = me ? (z | c_conf) : z;
-                    usedbits |= me ? 1u : 0u;
-                    const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
-                    const bool crossed = (my_t <= ov) & (my_t > nv);
-                    atomicAnd((unsigned long long *)&Mw[(lane & (K - 1)) * 2 + (lane >> 5)],
-                              crossed ? ~(1ull << l) : ~0ull);
-                    placed |= 1ull << ti;
-                    my_assign = lane == ti ? gbase * 64 + l : my_assign;
-                    if (STAT_ON) st_hits++;
-                }
-            }
-        } else
-        // Exact first fit, container by container in FFD order; group g's records are
-        // read and written in registers through a wave-uniform index.
-        {
-            while (todo) {
-                const uint32_t ti = (uint32_t)__builtin_ctzll(todo);
-                todo &= todo - 1;
-                const uint32_t c_cpu = __builtin_amdgcn_readlane(cpu, ti);
-                const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
-                const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
-                const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
-                uint32_t cc = __builtin_amdgcn_readlane(cand, ti);  // != 0 for a todo container
-                uint32_t g, x, y, z;
-                uint64_t m, done;
-                // one exit (a match, or no candidate left): a loop with a second exit for
-                // the match gets a merged flag and eight more scalar ops per check
-                do {
-                    g = (uint32_t)__builtin_ctz(cc);
-                    cc &= cc - 1;
-                    x = rcf[g]; y = rmf[g]; z = rcu[g];
-                    const uint32_t lb = rlab[g];
-                    if (STAT_ON) st_checks++;
-                    // one v_cmp per condition straight into a scalar mask, ANDed on the
-                    // SALU (a single ballot of the combined bool costs two extra
-                    // dependent VALU ops on the chain)
-                    m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
-                        __builtin_amdgcn_ballot_w64(((lb & c_req) | (z & c_conf)) == 0u);
-                    // exit flag = m | (cc == 0), kept on the SALU (the compiler moves the 64-bit
-                    // test to the VALU otherwise)
-                    asm("s_cmp_eq_u32 %1, 0\n\ts_cselect_b64 %0, 1, 0\n\ts_or_b64 %0, %0, %2"
-                        : "=&s"(done) : "s"(cc), "s"(m) : "scc");
-                } while (done == 0u);
-                if (m) {
-                    // placement, branch-free: lane l's record changes; one all-lane
-                    // ds_and_b64 clears the crossed buckets (lanes 0-31 cpu masks,
-                    // lanes 32-63 mem masks of group g)
-                    const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                    const uint32_t oc = __builtin_amdgcn_readlane(x, l);
-                    const uint32_t om = __builtin_amdgcn_readlane(y, l);
-                    const uint32_t nc = oc - c_cpu, nm = om - c_mem;
-                    const uint32_t ux = (uint32_t)fp_writelane((int)nc, (int)l, (int)x);
-                    const uint32_t uy = (uint32_t)fp_writelane((int)nm, (int)l, (int)y);
-                    const uint32_t uz = (uint32_t)fp_writelane((int)(__builtin_amdgcn_readlane(z, l) | c_conf), (int)l, (int)z);
-                    // keep the three indexed writes adjacent: one s_set_gpr_idx window
-                    __builtin_amdgcn_sched_barrier(0);
-                    rcf[g] = ux;
-                    rmf[g] = uy;
-                    rcu[g] = uz;
-                    __builtin_amdgcn_sched_barrier(0);
-                    const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
-                    const bool crossed = (my_t <= ov) & (my_t > nv);
-                    atomicAnd((unsigned long long *)&Mw[(size_t)g * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
-                              crossed ? ~(1ull << l) : ~0ull);
-                    usedbits = (uint32_t)fp_writelane(
-                        (int)(__builtin_amdgcn_readlane(usedbits, l) | (1u << g)), (int)l, (int)usedbits);
-                    placed |= 1ull << ti;
-                    my_assign = (uint32_t)fp_writelane((int)((gbase + g) * 64 + l), (int)ti, (int)my_assign);
-                    if (STAT_ON) st_hits++;
-                }
-            }
-        }
-#else
         // Exact first fit, GROUP-major.  Container t's checks must see every earlier
         // container's placement in the group being checked, and nothing else matters to
         // it: placements in other groups touch other nodes.  So instead of walking the
@@ -854,74 +642,18 @@ k_ffd_pipe(const PipeArgs a) {
         // s_set_gpr_idx windows, no indexed copies).
         {
             uint32_t nxt = ((todo >> lane) & 1ull) ? (cand ? (uint32_t)__builtin_ctzll((uint64_t)cand) : G) : G;
-#ifndef FP_NO_ASM
             // the hand-scheduled loop of fp_pipe_asm.h, one asm block per (static) group;
             // one-group stages leave their bucket masks at the tile's start state (still
             // exact: a stale mask is a superset): config 3 (1 x 1M x 100k) ran 127 -> 104 ms
             // without the update, while config 4's 20-group stages need it (57 vs 66 ms)
             uint32_t nchk = 0, nhit = 0;
-            if (!FP_TODO_SKIP || todo)
-            fpp_groups<G, (G > 1), gbound>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
-                                   used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
-                                   (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
-                                   __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gmc, gmm);
+            if (todo)
+                fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+                                       used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
+                                       (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
+                                       __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
-#else
-#pragma unroll
-            for (uint32_t g = 0; g < G; ++g) {
-                uint64_t q = __builtin_amdgcn_ballot_w64(nxt == g);
-                while (q) {
-                    const uint32_t ti = (uint32_t)__builtin_ctzll(q);
-                    q &= q - 1;
-                    const uint32_t c_cpu = __builtin_amdgcn_readlane(cpu, ti);
-                    const uint32_t c_mem = __builtin_amdgcn_readlane(mem, ti);
-                    const uint32_t c_req = __builtin_amdgcn_readlane(req, ti);
-                    const uint32_t c_conf = __builtin_amdgcn_readlane(conf, ti);
-                    const uint32_t x = rcf[g], y = rmf[g], z = rcu[g];
-                    if (STAT_ON) st_checks++;
-                    const uint64_t m = __builtin_amdgcn_ballot_w64(x >= c_cpu) & __builtin_amdgcn_ballot_w64(y >= c_mem) &
-                                       __builtin_amdgcn_ballot_w64(((rlab[g] & c_req) | (z & c_conf)) == 0u);
-                    if (m) {
-                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                        const uint32_t oc = __builtin_amdgcn_readlane(x, l);
-                        const uint32_t om = __builtin_amdgcn_readlane(y, l);
-                        const uint32_t nc = oc - c_cpu, nm = om - c_mem;
-                        const bool me = lane == l;
-                        rcf[g] = me ? nc : x;
-                        rmf[g] = me ? nm : y;
-                        rcu[g] = me ? (z | c_conf) : z;
-                        if (g < 32) usedbits |= me ? (1u << g) : 0u;
-                        else used_hi |= me ? (1u << (g & 31)) : 0u;
-                        // bucket masks: lanes 0-31 hold the cpu thresholds, 32-63 the mem ones;
-                        // clear bit l where the placement crossed the threshold
-                        const uint32_t ov = lane < (uint32_t)K ? oc : om, nv = lane < (uint32_t)K ? nc : nm;
-                        const bool crossed = (my_t <= ov) & (my_t > nv);
-                        atomicAnd((unsigned long long *)&Mw[(size_t)g * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
-                                  crossed ? ~(1ull << l) : ~0ull);
-                        placed |= 1ull << ti;
-                        my_assign = (uint32_t)fp_writelane((int)((gbase + g) * 64 + l), (int)ti, (int)my_assign);
-                        if (STAT_ON) st_hits++;
-                    } else {
-                        // later candidate groups of container ti (none: it leaves the tile)
-                        const uint64_t cl = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cand, ti);
-                        const uint64_t ch = (uint32_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)cand >> 32), ti);
-                        const uint64_t cc = ((ch << 32) | cl) & ~((2ull << g) - 1ull);
-                        nxt = (uint32_t)fp_writelane((int)(cc ? (uint32_t)__builtin_ctzll(cc) : G), (int)ti, (int)nxt);
-                        if (STAT_ON) {
-                            const uint64_t mc = __builtin_amdgcn_ballot_w64(x >= c_cpu);
-                            const uint64_t mm = __builtin_amdgcn_ballot_w64(y >= c_mem);
-                            const uint64_t ml = __builtin_amdgcn_ballot_w64((rlab[g] & c_req) == 0u);
-                            st_miss[0] += (mc & mm) != 0;
-                            st_miss[1] += (mc & mm & ml) != 0;
-                            st_miss[2] += mc != 0 && !(mc & mm);
-                            st_miss[3] += mm != 0 && !(mc & mm);
-                        }
-                    }
-                }
-            }
-#endif
         }
-#endif
         if (zs_g < G) {
             // all-zero containers change no record: each takes the first schedulable node
             const uint64_t zm = __builtin_amdgcn_ballot_w64(zero);
@@ -1095,12 +827,11 @@ k_ffd_pipe(const PipeArgs a) {
         atomicAdd(&CNT[1], n_rej);
         STAT_ADD(st_slot, 0, st_visits); STAT_ADD(st_slot, 1, st_checks); STAT_ADD(st_slot, 2, st_hits);
         STAT_ADD(st_slot, 3, st_batches); STAT_ADD(st_slot, 4, st_spin_in); STAT_ADD(st_slot, 5, st_spin_out);
-        STAT_ADD(st_slot, 6, st_miss[0]); STAT_ADD(st_slot, 7, st_miss[1]); STAT_ADD(st_slot, 14, st_miss[2]); STAT_ADD(st_slot, 15, st_miss[3]);
         STAT_ADD(st_slot, 8, ck_in); STAT_ADD(st_slot, 9, ck_pre); STAT_ADD(st_slot, 10, ck_cand); STAT_ADD(st_slot, 11, ck_fwd);
         STAT_ADD(st_slot, 12, ck_wait); STAT_ADD(st_slot, 13, STAT_CLK() - ck_t0);
     }
     (void)ck_t0; (void)ck_in; (void)ck_pre; (void)ck_cand; (void)ck_fwd; (void)ck_wait;
-    (void)st_miss; (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
+    (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
     // write the tile's node state back (registers -> HBM)
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
@@ -1472,21 +1203,15 @@ static const launch_fn kLaunch[MAX_G + 1] = {
 // one-wave segments (W = 1) of 13..40 groups: G rounded up to a multiple of 4 (the padding
 // groups hold unschedulable records, which no container fits)
 constexpr uint32_t MAX_G_WIDE = 40;
-#ifndef FP_LEGACY_LOOP
 static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {
-    nullptr, nullptr, nullptr, FP_WIDE12_WAVES ? launch_g<12, 64> : nullptr, launch_g<16, 64>, launch_g<20, 64>,
+    nullptr, nullptr, nullptr, launch_g<12, 64>, launch_g<16, 64>, launch_g<20, 64>,
     launch_g<24, 64>, launch_g<28, 64>, launch_g<32, 64>, launch_g<36, 64>, launch_g<40, 64>};
 static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {
-    nullptr, nullptr, nullptr, FP_WIDE12_WAVES ? (const void *)k_ffd_pipe<12, 64> : nullptr,
+    nullptr, nullptr, nullptr, (const void *)k_ffd_pipe<12, 64>,
     (const void *)k_ffd_pipe<16, 64>, (const void *)k_ffd_pipe<20, 64>,
     (const void *)k_ffd_pipe<24, 64>, (const void *)k_ffd_pipe<28, 64>, (const void *)k_ffd_pipe<32, 64>,
     (const void *)k_ffd_pipe<36, 64>, (const void *)k_ffd_pipe<40, 64>};
-static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && (G > 12 || (FP_WIDE12_WAVES && G == 12)); }
-#else  // round 1's loops take at most 16 groups per stage
-static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {nullptr};
-static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {nullptr};
-static inline bool wide_g(uint32_t, uint32_t) { return false; }
-#endif
+static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G >= 12; }
 
 }  // namespace fpp
 
@@ -1540,7 +1265,7 @@ bool fp_pipe_plan(const fp_ctx *c, uint32_t S, uint32_t N, uint32_t *G_out, uint
     // same time while a scenario needs fewer registers than with 4-stage segments.
     const bool narrow = (uint64_t)S * NG <= kNarrowWaves;
     // one-wave segments hold at most 12 groups (96 VGPRs at five waves per SIMD, 20
-    // segments in flight per CU; FP_WIDE12_WAVES).  With lagged segment tickets (the kernel) a segment runs
+    // segments in flight per CU; WIDE12_WAVES).  With lagged segment tickets (the kernel) a segment runs
     // on complete input, so more, smaller segments keep more waves busy: config 4 (79
     // groups) 7 segments of 12 groups 28.3 ms, 10 of 8 groups 28.2, 4 of 20 groups 30.3,
     // 3 of 24-28 groups 30.2.  (Without the lag, when a segment waited on its upstream
@@ -1644,11 +1369,11 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     if (B <= 1) g->bounded = 0;
     g->slots = g->bounded ? (ring < full ? ring : full) : full;
     // systolic group fill (fp_pipe_sys.h): queues of at least this many containers (compiled for
-    // stages of at most FP_SYS_MAX_G groups)
+    // stages of at most SYS_MAX_G groups)
     // Default: queues of >= 32 containers in the narrow stages (configs 2 / 3 / 5: one scenario,
     // one-group stages); config 3's k_ffd_pipe 72.1 -> 65.2 ms, config 2 0.81 -> 0.75 ms, every
     // threshold from 1 to 48 within 1 % (tools/sys_sweep.py, profiles/r03c_sys_sweep.jsonl)
-    g->sys = G <= FP_SYS_MAX_G ? (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 32) : 0u;
+    g->sys = G <= SYS_MAX_G ? (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 32) : 0u;
     if (g->sys > 64) g->sys = 64;
     g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
     if (g->sys_extra > 128) g->sys_extra = 128;

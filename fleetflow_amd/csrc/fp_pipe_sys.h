@@ -34,10 +34,6 @@ namespace fpp {
 __device__ unsigned long long g_sys_stats[8];
 #endif
 
-// DPP wave_ror:1 -- lane i receives lane i-1, lane 0 receives lane 63
-__device__ __forceinline__ uint32_t sys_ror1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x13C, 0xF, 0xF, false);
-}
 __device__ __forceinline__ uint32_t sys_push(uint32_t dst_lane, uint32_t v) {  // ds_permute_b32
     return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst_lane << 2), (int)v);
 }
@@ -55,57 +51,9 @@ __device__ __forceinline__ uint32_t sys_wave_or(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
-// A/B variant (slower: config 3 65.2 vs 64.3 ms, profiles/r03ah_stair_ab.jsonl): the systolic
-// calls' live sets hold 12.5 nodes, 12.0 of them useful (r03ah_systolic_stats.jsonl)
-#ifndef FP_SYS_STAIR
-#define FP_SYS_STAIR 0
-#endif
-// A/B variants.  FP_SYS_MISS_EXIT: the step loop ends at its first miss (a container that tested
-// every live position), and the containers still pending go to the serial finish.
-// FP_SYS_LEFT_REFILTER: that finish re-tests the queue after each miss (fpp_refilter_loop).
-// Config 3 (profiles/r03ai_systolic_exit_ab.jsonl): default 64.2 / 63.9 ms, re-test finish 63.6
-// (alternated twice in r03ak_left_refilter_ab.jsonl: 64.1 / 63.7 vs 64.1 / 64.1, no difference),
-// miss exit 66.8 with the re-test and 67.5 without: a miss inside the step loop costs one lane of
-// a step, less than any serial check of it afterwards.
-#ifndef FP_SYS_MISS_EXIT
-#define FP_SYS_MISS_EXIT 0
-#endif
-#ifndef FP_SYS_LEFT_REFILTER
-#define FP_SYS_LEFT_REFILTER 0
-#endif
-#if FP_SYS_MISS_EXIT
-#define FPP_SYS_MISS_TEST "s_bitcmp1_b64 %[pend], %[u]\n\t" "s_cbranch_scc1 .LsysMiss%=\n\t"
-#else
-#define FPP_SYS_MISS_TEST ""
-#endif
-// The live nodes that dominate some queued container in (cpu, mem) -- the queue's staircase.
-// Queued lanes hold non-increasing cpu (FFD order); lane t is a staircase point when its mem is
-// below every later queued lane's.  Every queued container is dominated by a staircase point at or
-// after it (the last lane holding the minimum mem of its suffix), so a node outside the result fits
-// no queued container, now or after any placement: dropping it from the live set is exact.
-__device__ __forceinline__ uint64_t sys_stair(uint64_t q, uint32_t cpu, uint32_t mem, uint32_t rcf, uint32_t rmf) {
-    const uint32_t lane = __lane_id();
-    const uint32_t m = ((q >> lane) & 1ull) ? mem : 0xFFFFFFFFu;
-    // min over the later lanes: reverse the lanes, exclusive prefix min (wave_shr:1, then the row
-    // scan of wave_min), reverse back
-    const uint32_t r = sys_pull(63u - lane, m);
-    uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)r, 0x138, 0xF, 0xF, false);  // wave_shr:1
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x111, 0xF, 0xF, false));      // row_shr:1
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x112, 0xF, 0xF, false));      // row_shr:2
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x114, 0xF, 0xF, false));      // row_shr:4
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x118, 0xF, 0xF, false));      // row_shr:8
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x142, 0xA, 0xF, false));      // row_bcast:15
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x143, 0xC, 0xF, false));      // row_bcast:31
-    const uint32_t later = sys_pull(63u - lane, x);
-    uint64_t pts = __builtin_amdgcn_ballot_w64(((q >> lane) & 1ull) && m < later);
-    bool useful = false;
-    while (pts) {
-        const uint32_t t = (uint32_t)__builtin_ctzll(pts);
-        pts &= pts - 1;
-        useful |= (rcf >= __builtin_amdgcn_readlane(cpu, t)) & (rmf >= __builtin_amdgcn_readlane(mem, t));
-    }
-    return __builtin_amdgcn_ballot_w64(useful);
-}
+// (Measured and removed in round 4, numbers in DESIGN.md 4.3: narrowing the live set to the
+// queue's (cpu, mem) staircase, 65.2 vs 64.3 ms on config 3; ending the step loop at its first
+// miss, 66.8 vs 64 ms; re-testing the serial finish after each miss, no difference.)
 
 // One group's queue q (lanes = containers in FFD order; cpu/mem/req/conf per lane) against
 // the group's records (lane = node: rcf, rmf, rcu, rlab = ~labels).  qc/qm: the batch's
@@ -113,7 +61,7 @@ __device__ __forceinline__ uint64_t sys_stair(uint64_t q, uint32_t cpu, uint32_t
 // Returns in asg the node (gbg | l) of every placed queued lane and FP_NONE for the others
 // of q (left for the caller: misses, or `left` = still pending for the serial finish);
 // touched |= the nodes placed on.
-// The step loop (exact semantics of the FP_SYS_CXX loop above it in fpp_sys_group).
+// The step loop.
 // Phase A (tau < L): the window of started containers grows by one lane per step,
 // win = lanes 0..tau.  Phase B (tau >= L): it slides, win = lanes tau-L+1..tau, and
 // container tau - L, which has tested every live position, leaves `pend` (a miss).
@@ -158,7 +106,6 @@ __device__ __forceinline__ void fpp_sys_steps(uint32_t &xc, uint32_t &xm, uint32
         "s_cmp_ge_u32 %[tau], %[cap]\n\t"
         "s_cbranch_scc1 .LsysEnd%=\n\t"
         "s_lshl_b64 %[win], %[win], 1\n\t"
-        FPP_SYS_MISS_TEST
         "s_bitset0_b64 %[pend], %[u]\n\t"
         "s_add_u32 %[u], %[u], 1\n\t"
         "s_and_b64 exec, %[win], %[pend]\n\t"
@@ -178,10 +125,7 @@ __device__ __forceinline__ void fpp_sys_steps(uint32_t &xc, uint32_t &xm, uint32
         "v_mov_b32_dpp %[xc], %[xc] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_mov_b32_dpp %[xm], %[xm] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_mov_b32_dpp %[xu], %[xu] wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
-        "s_cbranch_scc1 .LsysB%=\n\t"
-        "s_branch .LsysEnd%=\n"
-        ".LsysMiss%=:\n\t"  // container u tested every position: a miss; stop here
-        "s_bitset0_b64 %[pend], %[u]\n"
+        "s_cbranch_scc1 .LsysB%=\n"
         ".LsysEnd%=:\n\t"
         "s_mov_b64 exec, %[esv]"
         : [xc] "+v"(xc), [xm] "+v"(xm), [xu] "+v"(xu), [xl] "+v"(xl), [apos] "+v"(apos), [pend] "+s"(pend),
@@ -205,8 +149,7 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     SysOut out{0};
     // live nodes: the batch corner (a node outside it fits no container of the batch, now or
     // later) -> positions 0..L-1, in node order
-    uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
-    if (FP_SYS_STAIR && lm) lm &= sys_stair(q, cpu, mem, rcf, rmf);
+    const uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
     const uint32_t L = (uint32_t)__builtin_popcountll(lm);
     if (L == 0) {  // nothing can fit: every queued container misses the group
         if ((q >> lane) & 1ull) asg = 0xFFFFFFFFu;
@@ -232,34 +175,7 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     uint64_t pend = Q >= 64 ? ~0ull : ((1ull << Q) - 1ull);  // compacted containers still open
     uint32_t tau = 0;                                         // steps taken = rotations applied
     uint32_t apos = 0xFFFFFFFFu;                              // step of the placement (compacted lane)
-#ifdef FP_SYS_CXX
-    uint64_t started = 0;
-    while (true) {
-        if (tau < 64) started |= 1ull << tau;
-        if (tau >= L && tau - L < 64) pend &= ~(1ull << (tau - L));  // tested every position: a miss
-        if (!pend || tau >= max_steps) break;
-        const uint64_t act = pend & started;
-        const uint64_t f1 = __builtin_amdgcn_ballot_w64(xc >= kc);
-        const uint64_t f2 = __builtin_amdgcn_ballot_w64(xm >= km);
-        const uint64_t f3 = __builtin_amdgcn_ballot_w64(((xl & kr) | (xu & kx)) == 0u);
-        const uint64_t fit = act & f1 & f2 & f3;
-        if ((fit >> lane) & 1ull) {
-            xc -= kc;
-            xm -= km;
-            xu |= kx;
-            apos = tau;
-        }
-        pend &= ~fit;
-        ++tau;
-        xc = sys_ror1(xc);
-        xm = sys_ror1(xm);
-        xu = sys_ror1(xu);
-        xl = sys_ror1(xl);
-    }
-    if (tau >= L && tau - L < 64) pend &= ~(1ull << (tau - L));
-#else
     fpp_sys_steps(xc, xm, xu, xl, kc, km, kr, kx, apos, pend, tau, L, max_steps);
-#endif
 #ifdef FP_PIPE_STATS
     {
         // live nodes some queued container fits at the batch-start state (before the steps: the
@@ -333,12 +249,7 @@ __device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint
                           : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap);
     uint64_t left = fpp_uniform64(so.left);
     touched = fpp_uniform64(touched);
-    if (left) {
-        if (FP_SYS_LEFT_REFILTER)
-            fpp_refilter_loop(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk, qc, qm);
-        else
-            fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
-    }
+    if (left) fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
     const uint32_t lane = __lane_id();
     const bool inq = (q >> lane) & 1ull;
     const uint64_t hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);
