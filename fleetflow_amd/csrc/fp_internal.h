@@ -1,5 +1,6 @@
 // fp_internal.h -- shared internals of libfleetplace.so (HIP, gfx950 only).
 #pragma once
+#include <cmath>
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -111,7 +112,21 @@ size_t fp_pipe_ws_bytes(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N);
 int fp_place_ws_bytes_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint64_t *bytes);
 // bucket thresholds of the candidate masks: K ascending values, T[0] = 0
 constexpr int FP_BUCKETS = 32;
-void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T);  // geometric from lo to hi
+// geometric from lo to hi (host and device: fp_place.hip k_thresholds)
+__host__ __device__ inline void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
+    T[0] = 0;
+    if (lo == 0) lo = 1;
+    if (hi < lo) hi = lo;
+    const double r = pow((double)hi / (double)lo, 1.0 / (double)(FP_BUCKETS - 2));
+    double v = (double)lo;
+    for (int k = 1; k < FP_BUCKETS; ++k) {
+        uint32_t x = k == FP_BUCKETS - 1 ? hi : (uint32_t)ceil(v);
+        if (x < T[k - 1]) x = T[k - 1];
+        if (x > hi) x = hi;
+        T[k] = x;
+        v *= r;
+    }
+}
 // the FFD-sorted SoA [S][C] the pipeline streams (fp_pipe.hip)
 struct fp_pipe_soa {
     uint32_t *s_cpu, *s_mem, *s_req, *s_conf, *s_idx;
@@ -120,11 +135,12 @@ int fp_pipe_soa_take(fp_ctx *c, size_t SC, fp_pipe_soa *soa);
 // 1 when the position word carries the bucket indices (bits 21-30)
 uint32_t fp_pipe_kpack(const fp_ctx *c, uint32_t C);
 // ready: the per-scenario LDS sort already wrote order, s_cpu, s_mem and s_idx (only the
-// req / conf / CYCLE gather remains); null: gather everything from order + sorted keys
+// req / conf / CYCLE gather remains); null: gather everything from order + sorted keys.
+// thr: the pipeline's bucket thresholds in device memory ([FP_BUCKETS] cpu, then mem)
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
-                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
-                   const uint32_t *tm, const fp_pipe_soa *ready);
+                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *thr,
+                   const fp_pipe_soa *ready);
 
 // ---- device helpers ----
 namespace fpd {

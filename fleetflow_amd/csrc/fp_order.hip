@@ -98,21 +98,29 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(const uint8_t *__restri
 }
 
 // ---- levelize -----------------------------------------------------------------
+// A corrupt CSR raises FP_ECORRUPT in the (sticky) error word AND this call's own `bad` word:
+// every later kernel of the call reads `bad` and does nothing, so no expansion runs on an
+// invalid graph and the host never waits for the check (fp_dev_levelize stays asynchronous).
+__device__ __forceinline__ void lv_corrupt(uint32_t *err, uint32_t *bad) {
+    atomicMax(err, (uint32_t)(-FP_ECORRUPT));
+    atomicOr(bad, 1u);
+}
+
 __global__ void k_check_csr(const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t E,
-                            uint32_t *__restrict__ err) {
+                            uint32_t *__restrict__ err, uint32_t *__restrict__ bad) {
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v < V) {
-        if (row_ptr[v + 1] < row_ptr[v]) atomicMax(err, (uint32_t)(-FP_ECORRUPT));
+        if (row_ptr[v + 1] < row_ptr[v]) lv_corrupt(err, bad);
     }
-    if (v == 0 && (row_ptr[0] != 0 || row_ptr[V] != E)) atomicMax(err, (uint32_t)(-FP_ECORRUPT));
+    if (v == 0 && (row_ptr[0] != 0 || row_ptr[V] != E)) lv_corrupt(err, bad);
 }
 
 __global__ void k_indeg(const uint32_t *__restrict__ col, uint32_t E, uint32_t V,
-                        uint32_t *__restrict__ indeg, uint32_t *__restrict__ err) {
+                        uint32_t *__restrict__ indeg, uint32_t *__restrict__ err, uint32_t *__restrict__ bad) {
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
          e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t v = col[e];
-        if (v >= V) atomicMax(err, (uint32_t)(-FP_ECORRUPT));
+        if (v >= V) lv_corrupt(err, bad);
         else atomicAdd(&indeg[v], 1u);
     }
 }
@@ -157,8 +165,9 @@ __global__ void k_expand(const uint32_t *__restrict__ frontier, const uint32_t *
 }
 
 __global__ void k_lvl_final(const uint32_t *__restrict__ indeg, uint32_t V, uint32_t cyc_key,
-                            uint32_t *__restrict__ level, uint32_t *__restrict__ keys,
-                            uint32_t *__restrict__ vals, uint32_t *__restrict__ ncyc) {
+                            uint32_t *__restrict__ level, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                            uint32_t *__restrict__ ncyc, uint32_t *__restrict__ ck) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ck = cyc_key;
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool cyc = v < V && indeg[v] != 0;
     if (v < V) {
@@ -218,7 +227,9 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // and the rest of each passed vertex's edges goes to the queue as a partial item.  A chain of
 // depth D takes ~D / kHops rounds.  (Two levels per round: config-5 levelize 1.51 -> 1.13 ms.)
 __global__ void k_edge_rec(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t E,
-                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec) {
+                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec,
+                           const uint32_t *__restrict__ bad) {
+    if (*bad) return;
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t w = col[e];
         rec[e] = w < V ? make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u)
@@ -231,7 +242,8 @@ __global__ void k_edge_rec(const uint32_t *__restrict__ row_ptr, const uint32_t 
 // first edge -- one dependent 16-B load per edge and hop, instead of chasing col / row_ptr.
 // A hop is kept only while every edge before it is an only-parent edge (zero record otherwise).
 __global__ void k_edge_hop(uint32_t E, const uint4 *__restrict__ rec, const uint4 *__restrict__ prev,
-                           uint4 *__restrict__ next) {
+                           uint4 *__restrict__ next, const uint32_t *__restrict__ bad) {
+    if (*bad) return;
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint4 r = rec[e];
         const uint4 p = prev ? prev[e] : r;  // the hop before (the child itself for the first hop)
@@ -247,7 +259,8 @@ __global__ void k_edge_hop(uint32_t E, const uint4 *__restrict__ rec, const uint
 __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
                                  const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t *__restrict__ level,
                                  uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
-                                 bool pk) {
+                                 bool pk, const uint32_t *__restrict__ bad) {
+    if (*bad) return;
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = v < V;
     uint32_t l0 = 0, deg = 0;
@@ -275,7 +288,9 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
 __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
                                                   const uint4 *__restrict__ erec2, uint32_t E, uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
                                                   uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
-                                                  uint32_t *__restrict__ err, bool pk) {
+                                                  uint32_t *__restrict__ err, bool pk,
+                                                  const uint32_t *__restrict__ bad) {
+    if (*bad) return;  // a corrupt CSR: no expansion (uniform: every block leaves)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sh = blockIdx.x % kShards;
     uint32_t *head = &ctl[sh * kCtlStride];
@@ -571,41 +586,84 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
 }
 
 // level -> sort keys; vertices never finished (cycle members and everything behind
-// them) are NONE and take cyc_key; counts them.
-__global__ void k_lvl_async_final(uint32_t V, uint32_t cyc_key, const uint32_t *__restrict__ level,
-                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                                  uint32_t *__restrict__ ncyc) {
+// them) are NONE and take the cycle key, which sorts after every level: max(largest level, 1)
+// + 1, from the largest level the async kernel recorded (ctl maxlvl), computed here on the
+// device and left in *ck for the sort; counts the NONE vertices.
+__global__ void k_lvl_async_final(uint32_t V, const uint32_t *__restrict__ ctl, const uint32_t *__restrict__ level,
+                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t *__restrict__ ncyc,
+                                  uint32_t *__restrict__ ck,
+                                  const uint32_t *__restrict__ bad) {
+    if (*bad) return;
+    const uint32_t maxl = ctl[26 * kCtlStride];
+    const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ck = cyc_key;
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool cyc = v < V && level[v] == FP_NONE;
     if (v < V) {
         keys[v] = cyc ? cyc_key : level[v];
-        vals[v] = (uint32_t)v;
+        vals[v] = (uint32_t)v;  // the radix fallback's values (the counting sort's scratch)
     }
     const uint64_t m = __ballot(cyc);
     if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(ncyc, (uint32_t)__popcll(m));
 }
 
 // ---- stable counting sort of the level keys (the start order) ----------------------------
-// keys[v] < nb <= CS_BINS, order = stable sort of 0..V-1 by key.  Three small launches instead
-// of rocprim's ~21 radix passes (launch-bound at config 5's 1M keys: 0.16 ms):
-//   k_cs_hist    per tile of CS_TILE keys: a histogram in LDS -> hist[tile][bin]
+// LSD over CS_BITS-bit digits: pass p orders by bits [p * CS_BITS, (p + 1) * CS_BITS) of the key,
+// stably, so after the last pass the vertices are in (level, index) order.  Three small launches
+// per pass instead of rocprim's ~21 radix launches (launch-bound at config 5's 1M keys: 0.16 ms):
+//   k_cs_hist    per tile of CS_TILE keys: a histogram of the pass's digit in LDS -> hist[tile][bin]
 //   k_cs_scan    one workgroup: hist[tile][bin] <- bin base + keys of the bin in earlier tiles
 //   k_cs_scatter per tile: per-wave counts of each wave's contiguous slice, then each wave walks
-//                its slice in order, 64 keys at a time, ranking equal keys by a ballot match mask
-//                (the same stable scheme as fp_place.hip's per-scenario sort)
-constexpr uint32_t CS_TILE = 16384, CS_BINS = 1024, CS_WAVES = 16, CS_MAX_TILES = 1024;
-__global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t nb,
-                                                  uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[CS_BINS];
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
-    __syncthreads();
-    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
-    for (uint32_t i = threadIdx.x; i < CS_TILE && t0 + i < V; i += blockDim.x) atomicAdd(&h[min(keys[t0 + i], nb - 1)], 1u);
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[(size_t)blockIdx.x * nb + b] = h[b];
+//                its slice in order, 64 keys at a time, ranking equal digits by a ballot match
+//                mask (the same stable scheme as fp_place.hip's per-scenario sort)
+// The key range is a DEVICE value (*ck: the cycle key, the largest key): a pass beyond the digits
+// it needs returns at once, the last needed pass writes the vertex order to `order`, and earlier
+// passes ping-pong (key, vertex) pairs through two scratch pairs.  The host enqueues the passes V
+// could need (ceil(bits(V + 1) / CS_BITS)) and reads nothing back: config 5's 509 levels take one
+// pass and the others return at once.
+constexpr uint32_t CS_TILE = 16384, CS_BITS = 10, CS_BINS = 1u << CS_BITS, CS_WAVES = 16, CS_MAX_TILES = 1024;
+
+struct CsPass {
+    uint32_t sh, nb, nbits;  // digit shift, bins (digits < nb), bits the match masks test
+    bool active, last;
+};
+__device__ __forceinline__ CsPass cs_pass(uint32_t p, const uint32_t *ck) {
+    const uint32_t kmax = *ck;
+    const uint32_t bits = kmax ? 32u - (uint32_t)__builtin_clz(kmax) : 1u;
+    const uint32_t need = (bits + CS_BITS - 1u) / CS_BITS;
+    CsPass c;
+    c.sh = p * CS_BITS;
+    c.active = p < need;
+    c.last = p + 1u == need;
+    c.nb = c.last ? (kmax >> c.sh) + 1u : CS_BINS;
+    c.nbits = c.nb > 1u ? 32u - (uint32_t)__builtin_clz(c.nb - 1u) : 0u;
+    return c;
+}
+__device__ __forceinline__ uint32_t cs_digit(uint32_t key, const CsPass &c) {
+    return min(c.last ? key >> c.sh : (key >> c.sh) & (CS_BINS - 1u), c.nb - 1u);
 }
 
-__global__ __launch_bounds__(1024) void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t nb) {
+__global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t p,
+                                                  const uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
+                                                  uint32_t *__restrict__ hist) {
+    if (*bad) return;
+    const CsPass c = cs_pass(p, ck);
+    if (!c.active) return;
+    __shared__ uint32_t h[CS_BINS];
+    for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
+    for (uint32_t i = threadIdx.x; i < CS_TILE && t0 + i < V; i += blockDim.x) atomicAdd(&h[cs_digit(keys[t0 + i], c)], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) hist[(size_t)blockIdx.x * c.nb + b] = h[b];
+}
+
+__global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t p, const uint32_t *__restrict__ ck,
+                          const uint32_t *__restrict__ bad) {
+    if (*bad) return;
+    const CsPass c = cs_pass(p, ck);
+    if (!c.active) return;
+    const uint32_t nb = c.nb;
     __shared__ uint32_t tot[CS_BINS];
     const uint32_t b = threadIdx.x;  // one bin per thread (nb <= CS_BINS = blockDim)
     uint32_t run = 0;
@@ -645,9 +703,17 @@ __device__ __forceinline__ uint64_t cs_match(uint32_t v, bool valid, uint32_t nb
     return m;
 }
 
-__global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict__ keys, uint32_t V, uint32_t nb,
-                                                     uint32_t nbits, const uint32_t *__restrict__ off,
-                                                     uint32_t *__restrict__ order) {
+// pass p: (keys, vals) -> (kout, vout), or the vertices alone -> order on the last pass.
+// vals null: the vertex is the key's index (pass 0).
+__global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                     uint32_t V, uint32_t p, const uint32_t *__restrict__ ck,
+                                                     const uint32_t *__restrict__ bad, const uint32_t *__restrict__ off,
+                                                     uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
+                                                     uint32_t *__restrict__ vout) {
+    if (*bad) return;
+    const CsPass c = cs_pass(p, ck);
+    if (!c.active) return;
+    const uint32_t nb = c.nb;
     __shared__ uint32_t wh[CS_WAVES][CS_BINS];
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -656,7 +722,7 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
     const size_t t0 = (size_t)blockIdx.x * CS_TILE;
     const uint32_t slice = CS_TILE / CS_WAVES;
     const size_t s0 = t0 + (size_t)w * slice;
-    for (uint32_t i = lane; i < slice && s0 + i < V; i += 64) atomicAdd(&wh[w][min(keys[s0 + i], nb - 1)], 1u);
+    for (uint32_t i = lane; i < slice && s0 + i < V; i += 64) atomicAdd(&wh[w][cs_digit(keys[s0 + i], c)], 1u);
     __syncthreads();
     for (uint32_t b = t; b < nb; b += blockDim.x) {  // per bin: wave offsets in wave order
         uint32_t run = off[(size_t)blockIdx.x * nb + b];
@@ -670,13 +736,21 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
     for (uint32_t i0 = 0; i0 < slice && s0 + i0 < V; i0 += 64) {
         const size_t v = s0 + i0 + lane;
         const bool valid = i0 + lane < slice && v < V;
-        const uint32_t k = valid ? min(keys[v], nb - 1) : 0u;
-        const uint64_t m = cs_match(k, valid, nbits);
+        const uint32_t key = valid ? keys[v] : 0u;
+        const uint32_t k = valid ? cs_digit(key, c) : 0u;
+        const uint32_t x = valid ? (vals ? vals[v] : (uint32_t)v) : 0u;
+        const uint64_t m = cs_match(k, valid, c.nbits);
         const uint32_t o = wh[w][k];
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane's read before the update
         if (valid) {
             if ((m & lt) == 0) wh[w][k] = o + (uint32_t)__popcll(m);
-            order[o + (uint32_t)__popcll(m & lt)] = (uint32_t)v;
+            const uint32_t q = o + (uint32_t)__popcll(m & lt);
+            if (c.last) {
+                order[q] = x;
+            } else {
+                kout[q] = key;
+                vout[q] = x;
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
@@ -713,23 +787,29 @@ int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
     return FP_OK;
 }
 
-// order = stable sort of 0..V-1 by keys[] (keys <= cyc_key): the counting sort above when the
-// keys fit its bins and tiles, rocprim's radix sort otherwise (or with FP_OPT_LEVEL_SORT = 0).
-static int level_sort(hipStream_t st, bool counting, uint32_t *keys, uint32_t *keys_out, uint32_t *vals, uint32_t *order, uint32_t V,
-                      uint32_t cyc_key, void *tmp, size_t sort_tmp, uint32_t *cs_hist) {
-    const uint32_t nb = cyc_key + 1;
+// order = stable sort of 0..V-1 by keys[] (keys <= *ck, a device value): the LSD counting sort
+// above when its tiles cover V, else (or with FP_OPT_LEVEL_SORT = 0) rocprim's radix sort over all
+// 32 key bits (vals = the identity, k_lvl_*final).  No read-back either way.  Scratch: two
+// (key, vertex) pairs, kb[0]/vb[0] and kb[1]/vb[1].
+static int level_sort(hipStream_t st, bool counting, uint32_t *keys, uint32_t *const kb[2], uint32_t *const vb[2],
+                      uint32_t *order, uint32_t V, const uint32_t *ck, const uint32_t *bad, void *tmp,
+                      size_t sort_tmp, uint32_t *cs_hist) {
     const uint32_t ntiles = (uint32_t)(((size_t)V + CS_TILE - 1) / CS_TILE);
-    if (counting && nb <= CS_BINS && ntiles <= CS_MAX_TILES) {
-        k_cs_hist<<<ntiles, 1024, 0, st>>>(keys, V, nb, cs_hist);
-        FP_HIP(hipGetLastError());
-        k_cs_scan<<<1, CS_BINS, 0, st>>>(cs_hist, ntiles, nb);
-        FP_HIP(hipGetLastError());
-        k_cs_scatter<<<ntiles, 1024, 0, st>>>(keys, V, nb, fp_bitwidth(cyc_key), cs_hist, order);
-        FP_HIP(hipGetLastError());
+    if (counting && ntiles <= CS_MAX_TILES) {
+        const uint32_t passes = (fp_bitwidth((uint64_t)V + 1) + CS_BITS - 1) / CS_BITS;
+        for (uint32_t p = 0; p < passes; ++p) {
+            const uint32_t *ik = p ? kb[(p - 1) & 1] : keys;
+            const uint32_t *iv = p ? vb[(p - 1) & 1] : nullptr;
+            k_cs_hist<<<ntiles, 1024, 0, st>>>(ik, V, p, ck, bad, cs_hist);
+            FP_HIP(hipGetLastError());
+            k_cs_scan<<<1, CS_BINS, 0, st>>>(cs_hist, ntiles, p, ck, bad);
+            FP_HIP(hipGetLastError());
+            k_cs_scatter<<<ntiles, 1024, 0, st>>>(ik, iv, V, p, ck, bad, cs_hist, order, kb[p & 1], vb[p & 1]);
+            FP_HIP(hipGetLastError());
+        }
         return FP_OK;
     }
-    FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys, keys_out, vals, order, (size_t)V, 0, fp_bitwidth(cyc_key),
-                                     st));
+    FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys, kb[0], vb[1], order, (size_t)V, 0, 32, st));
     return FP_OK;
 }
 
@@ -772,16 +852,20 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     if (!indeg || !fa || !fb || !keys || !keys_out || !vals || !cnt || !ncyc || !tmp || (counting && !cs_hist))
         return FP_ENOMEM;
 
+    // ncyc[0]: cycle vertices; ncyc[4]: this call's corrupt-CSR flag (k_check_csr / k_indeg; every
+    // later kernel reads it and does nothing); ncyc[8]: the cycle key = the largest sort key
+    uint32_t *bad = ncyc + 4, *ck = ncyc + 8;
+    uint32_t *const kb[2] = {keys_out, fa}, *const vb[2] = {fb, vals};  // sort scratch; vals = identity
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_LEVEL, &ev);
     FP_HIP(hipMemsetAsync(indeg, 0, (size_t)V * 4, st));
     FP_HIP(hipMemsetAsync(cnt, 0, ncnt * 4, st));
     FP_HIP(hipMemsetAsync(ncyc, 0, 64, st));
-    k_check_csr<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, V, E, c->d_err);
+    k_check_csr<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, V, E, c->d_err, bad);
     FP_HIP(hipGetLastError());
     if (E) {
         k_indeg<<<blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192, 256, 0, st>>>(
-            g->col, E, V, indeg, c->d_err);
+            g->col, E, V, indeg, c->d_err, bad);
         FP_HIP(hipGetLastError());
     }
     if (!level_sync) {
@@ -797,30 +881,25 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
         const bool pk = V < (1u << 24);
         k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl,
-                                                             pk);
+                                                             pk, bad);
         FP_HIP(hipGetLastError());
-        // a corrupt CSR (k_check_csr / k_indeg) stops here, before any expansion
-        if ((rc = fp_take_err(c))) return rc;
         if (E) {
             const unsigned eg = blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192;
-            k_edge_rec<<<eg, 256, 0, st>>>(g->row_ptr, g->col, E, V, indeg, erec);
+            k_edge_rec<<<eg, 256, 0, st>>>(g->row_ptr, g->col, E, V, indeg, erec, bad);
             FP_HIP(hipGetLastError());
             for (uint32_t h = 0; h + 1 < kHops; ++h) {
-                k_edge_hop<<<eg, 256, 0, st>>>(E, erec, h ? erec2 + (size_t)(h - 1) * E : nullptr, erec2 + (size_t)h * E);
+                k_edge_hop<<<eg, 256, 0, st>>>(E, erec, h ? erec2 + (size_t)(h - 1) * E : nullptr, erec2 + (size_t)h * E,
+                                               bad);
                 FP_HIP(hipGetLastError());
             }
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
-            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err, pk);
+            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err, pk, bad);
             FP_HIP(hipGetLastError());
         }
-        FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &actl[26 * kCtlStride], 4, hipMemcpyDeviceToHost, st));
-        if ((rc = fp_take_err(c))) return rc;  // synchronises the read-back above too
-        const uint32_t maxl = ((uint32_t *)c->h_small)[2];
-        // levels <= max(maxl, 1); the cycle key sorts after every level
-        const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
-        k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, cyc_key, level, keys, vals, ncyc);
+        // the cycle key (from the largest level seen) is computed on the device: no read-back
+        k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, actl, level, keys, vals, ncyc, ck, bad);
         FP_HIP(hipGetLastError());
-        if ((rc = level_sort(st, counting, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
+        if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
         if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
@@ -853,9 +932,9 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     const uint32_t iters = L;
     // levels <= iters + 1; cycle key sorts after every level
     const uint32_t cyc_key = iters + 2;
-    k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, ncyc);
+    k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, ncyc, ck);
     FP_HIP(hipGetLastError());
-    if ((rc = level_sort(st, counting, keys, keys_out, vals, order, V, cyc_key, tmp, sort_tmp, cs_hist))) return rc;
+    if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
     if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
     fp_prof_end(c, FP_K_LEVEL, ev);
     return FP_OK;

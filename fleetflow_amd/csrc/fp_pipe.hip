@@ -100,7 +100,7 @@ struct PipeArgs {
     uint64_t *cost;
     uint32_t *err;
     uint64_t spin_ticks;    // deadlock guard, s_memrealtime ticks (100 MHz)
-    uint32_t tc[K], tm[K];  // ascending thresholds, tc[0] = tm[0] = 0
+    const uint32_t *thr;    // [2K] device: ascending thresholds, cpu then mem, thr[0] = thr[K] = 0
 };
 
 __device__ __forceinline__ uint32_t lds_acq(uint32_t *p) {
@@ -378,7 +378,7 @@ k_ffd_pipe(const PipeArgs a) {
     // ---- stage the tile into LDS and build the bucket masks ----
     // lane k < 32 holds Tc[k], lane 32 + k holds Tm[k] (K == 32: one wave covers both)
     static_assert(K == 32, "mask/threshold lane layout assumes K == 32");
-    const uint32_t my_t = lane < (uint32_t)K ? a.tc[lane] : a.tm[lane - K];
+    const uint32_t my_t = a.thr[lane];
     const uint32_t gbase = (b * W + w) * G;             // first (global) group of this tile
     uint64_t *Mw = M + (size_t)w * G * K * 2;           // the tile's masks
     // The tile's node records.  Unschedulable (and padding) nodes are stored so that every
@@ -883,10 +883,25 @@ __global__ __launch_bounds__(256) void k_node_summary(uint32_t N, const uint32_t
                                                       const uint8_t *__restrict__ sched, uint32_t *__restrict__ summ) {
     const size_t nb = (size_t)blockIdx.x * N;
     uint32_t u = 0, a = 0xFFFFFFFFu;
-    for (uint32_t n = threadIdx.x; n < N; n += blockDim.x) {
-        if (sched[nb + n]) {
-            u |= lab[nb + n];
-            a &= cu[nb + n];
+    // NS_U nodes per thread in flight (one block per scenario: a single load triple per thread at
+    // a time left the pass latency-bound, 0.23 ms for config 4's 4096 x 5k nodes)
+    constexpr uint32_t NS_U = 4;
+    for (uint32_t n0 = threadIdx.x; n0 < N; n0 += NS_U * blockDim.x) {
+        uint32_t l[NS_U], c[NS_U];
+        uint8_t sc[NS_U];
+#pragma unroll
+        for (uint32_t k = 0; k < NS_U; ++k) {
+            const uint32_t n = n0 + k * blockDim.x;
+            sc[k] = n < N ? sched[nb + n] : 0;
+            l[k] = n < N ? lab[nb + n] : 0u;
+            c[k] = n < N ? cu[nb + n] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < NS_U; ++k) {
+            if (sc[k]) {
+                u |= l[k];
+                a &= c[k];
+            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -908,14 +923,10 @@ __device__ __forceinline__ bool screened(const uint32_t *sm, uint32_t req, uint3
     return ((req & ~sm[0]) | (conf & sm[1])) != 0u;
 }
 
-// bucket thresholds for k_gather_sorted (by value: [0, K) cpu, [K, 2K) mem)
-struct GatherThr {
-    uint32_t t[2 * K];
-    uint32_t kpack;
-};
-
+// bucket thresholds for k_gather_sorted: thr [0, K) cpu, [K, 2K) mem (device), kpack as PipeArgs
 template <class KeyT>
-__global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
+__global__ void k_gather_sorted(const uint32_t *__restrict__ thr, uint32_t kpack, uint32_t S, uint32_t C,
+                                const uint32_t *__restrict__ order,
                                 const KeyT *__restrict__ skeys, uint32_t mbits, uint64_t cmax, uint64_t mmax,
                                 const uint32_t *__restrict__ cval, const uint32_t *__restrict__ mval,
                                 const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
@@ -933,7 +944,7 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
     const uint32_t lb = (gridDim.x & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t stride = blockDim.x;
     __shared__ uint32_t T[2 * K];
-    if (threadIdx.x < 2 * K) T[threadIdx.x] = th.t[threadIdx.x];
+    if (threadIdx.x < 2 * K) T[threadIdx.x] = thr[threadIdx.x];
     __syncthreads();
     // largest k with T[k] <= v (T ascending, T[0] = 0)
     auto bucket = [](const uint32_t *t, uint32_t v) {
@@ -996,7 +1007,7 @@ __global__ void k_gather_sorted(const GatherThr th, uint32_t S, uint32_t C, cons
                 __builtin_nontemporal_store(f[u], &s_conf[i]);
                 // the pipeline carries the SORTED position: its assign/reason stores land
                 // next to each other (k_unsort restores container order, coalesced)
-                const uint32_t kb = th.kpack ? (bucket(T, cv[u]) << 21) | (bucket(T + K, mv[u]) << 26) : 0u;
+                const uint32_t kb = kpack ? (bucket(T, cv[u]) << 21) | (bucket(T + K, mv[u]) << 26) : 0u;
                 __builtin_nontemporal_store(pos[u] | kb | cy[u], &s_idx[i]);
             }
         }
@@ -1217,21 +1228,6 @@ static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G >= 12; }
 
 using namespace fpp;
 
-void fp_thresholds(uint32_t lo, uint32_t hi, uint32_t *T) {
-    T[0] = 0;
-    if (lo == 0) lo = 1;
-    if (hi < lo) hi = lo;
-    const double r = pow((double)hi / (double)lo, 1.0 / (double)(K - 2));
-    double v = (double)lo;
-    for (int k = 1; k < K; ++k) {
-        uint32_t x = k == K - 1 ? hi : (uint32_t)ceil(v);
-        if (x < T[k - 1]) x = T[k - 1];
-        if (x > hi) x = hi;
-        T[k] = x;
-        v *= r;
-    }
-}
-
 // Pipeline geometry for N nodes: W waves (stages) of G groups per workgroup
 // (segment) and B segments per scenario.  One segment holds at most
 // MAX_SEG_GROUPS groups: 4 stages x 10 groups (20 KB of masks + rings).  Measured
@@ -1405,8 +1401,8 @@ int fp_pipe_soa_take(fp_ctx *c, size_t SC, fp_pipe_soa *soa) {
 
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
-                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *tc,
-                   const uint32_t *tm, const fp_pipe_soa *ready) {
+                   const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *thr,
+                   const fp_pipe_soa *ready) {
     PipeGeom geo;
     if (!pipe_geom(c, S, C, N, &geo)) return FP_EOVERFLOW;
     const uint32_t G = geo.G, W = geo.W, B = geo.B, R = geo.R, slots = geo.slots;
@@ -1429,10 +1425,6 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     FP_HIP(hipMemsetAsync(ctl, 0, 256 + nlinks * LCTL * 4, st));
     // buckets ride in s_idx when positions fit 21 bits (FP_OPT_KPACK = 0: search per stage)
     const uint32_t kpack = fp_pipe_kpack(c, C);
-    GatherThr gth;
-    memcpy(gth.t, tc, sizeof(uint32_t) * K);
-    memcpy(gth.t + K, tm, sizeof(uint32_t) * K);
-    gth.kpack = kpack;
     // stage-2 screen (k_node_summary): per-scenario label union / conflict intersection of the
     // schedulable nodes; FP_OPT_SCREEN = 0 sends every container through the pipeline
     uint32_t *summ = nullptr;
@@ -1465,11 +1457,11 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         if (g >= 64) g = (g + 7) & ~(size_t)7;  // a multiple of 8: XCD-contiguous mapping
         if (key_bytes == 4)
             k_gather_sorted<uint32_t><<<(unsigned)g, 256, 0, st>>>(
-                gth, S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
+                thr, kpack, S, C, order, (const uint32_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
                 b->conflict, b->level, summ, s_cpu, s_mem, s_req, s_conf, s_idx);
         else
             k_gather_sorted<uint64_t><<<(unsigned)g, 256, 0, st>>>(
-                gth, S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
+                thr, kpack, S, C, order, (const uint64_t *)skeys, mbits, cmax, mmax, cval, mval, b->cpu_m, b->mem_mib, b->req_labels,
                 b->conflict, b->level, summ, s_cpu, s_mem, s_req, s_conf, s_idx);
         FP_HIP(hipGetLastError());
     }
@@ -1499,10 +1491,9 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
         const int64_t pv = fp_opt(c, FP_OPT_LINK_PUBLISH, 32);
         a.publish = geo.bounded ? 1u : (uint32_t)(pv < 1 ? 1 : pv > 1024 ? 1024 : pv);
     }
-    // bucket thresholds (fp_place.hip chooses them; any ascending choice with T0 = 0 is
-    // exact -- it only decides how tight the candidate masks are)
-    memcpy(a.tc, tc, sizeof(a.tc));
-    memcpy(a.tm, tm, sizeof(a.tm));
+    // bucket thresholds (device; fp_place.hip k_thresholds chooses them -- any ascending choice
+    // with T0 = 0 is exact, it only decides how tight the candidate masks are)
+    a.thr = thr;
     const bool wide = wide_g(W, G);
     if (G < 1 || (wide ? (G > MAX_G_WIDE || G % 4) : G > MAX_G)) return FP_EOVERFLOW;
     hipEvent_t ev;

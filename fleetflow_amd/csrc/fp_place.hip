@@ -1,20 +1,19 @@
 // fp_place.hip -- stage 3: first-fit-decreasing placement, batched over what-if
 // scenarios (SPEC.md 2.3).  One workgroup owns one scenario.
 //
-// Pipeline per fp_dev_place_batch call:
-//   1. k_key_bounds : max(cpu_m), max(mem_mib) over the batch (exact key width)
-//   1b. k_value_bitmap + k_rank_tables: when both maxima are below 2^18, the distinct
-//                     cpu and mem values of the batch, so that a key field holds the
-//                     value's dense rank (order-preserving: the sort is unchanged)
-//   2. k_make_keys  : key = (scenario << kb) | ((cmask-c) << mb) | (mmask-m), c/m the
-//                     values or their ranks, value = container index; u32 keys when the
-//                     fields fit 32 bits, else u64.  Config 4 (512 scenarios, 79 cpu and
-//                     256 mem values): 9 + 7 + 8 = 24 bits -> three 8-bit radix passes
-//                     instead of five passes over 36-bit u64 keys
-//   3. rocprim radix sort (stable) => (cpu desc, mem desc, index asc) per scenario:
-//      segmented per scenario when there are several (no scenario bits in the key),
-//      device-wide otherwise (or with the scenario field above the key when
-//      FP_OPT_SEGSORT is 0).
+// Pipeline per fp_dev_place_batch call -- asynchronous: every data-dependent choice (dense ranks,
+// the LDS sort's eligibility, the key range, the bucket thresholds) is made on the device, so the
+// host enqueues the whole call without reading anything back.
+//   1. k_value_bitmap + k_rank_tables: the distinct cpu and mem values of the batch (values below
+//      2^18) as presence bitmaps -> dense ranks and ascending value tables; the raw bounds (max,
+//      smallest positive) in the same pass
+//   2. k_thresholds: the pipeline's bucket thresholds (spread over the distinct values, or
+//      geometric between the bounds) and the LDS sort's eligibility flag, into device memory
+//   3a. scenarios of at most ~50k containers (host-known): the per-scenario LDS sort below
+//      (k_digits + k_scen_sort), which falls back, in the same kernel, to a generic stable LSD
+//      sort of the raw values when the batch has more than 256 distinct values or values >= 2^18
+//   3b. larger scenarios: k_make_keys (full-width key (~cpu << 32 | ~mem), value = index) and a
+//      stable rocprim radix sort over 64 bits, segmented per scenario when there are several
 //   4. k_ffd_pipe   : (fp_pipe.hip) per scenario, containers in key order stream
 //                     through a pipeline of node-group stages (LDS-resident node
 //                     tiles); lowest feasible node wins, capacity updated in place.
@@ -25,8 +24,7 @@
 
 namespace {
 
-// out[0..1] = max(cpu), max(mem); out[2..3] = min positive cpu, mem (0xFFFFFFFF if none).
-// 16-byte loads, a block-level reduction in LDS and one set of atomics per block.
+// running max and smallest positive value of cpu (mc, lc) and mem (mm, lm)
 __device__ __forceinline__ void bounds_acc(uint32_t c, uint32_t m, uint32_t &mc, uint32_t &mm, uint32_t &lc,
                                            uint32_t &lm) {
     mc = max(mc, c);
@@ -35,47 +33,6 @@ __device__ __forceinline__ void bounds_acc(uint32_t c, uint32_t m, uint32_t &mc,
     lm = m ? min(lm, m) : lm;
 }
 
-__global__ __launch_bounds__(256) void k_key_bounds(const uint32_t *__restrict__ cpu,
-                                                    const uint32_t *__restrict__ mem, size_t n,
-                                                    uint32_t *__restrict__ out /* [4] */) {
-    uint32_t mc = 0, mm = 0, lc = 0xFFFFFFFFu, lm = 0xFFFFFFFFu;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(cpu) | reinterpret_cast<uintptr_t>(mem)) & 15u) == 0;
-    size_t head = 0;
-    if (aligned) {
-        const size_t n4 = n / 4;
-        const uint4 *c4 = reinterpret_cast<const uint4 *>(cpu), *m4 = reinterpret_cast<const uint4 *>(mem);
-        for (size_t i = t; i < n4; i += stride) {
-            const uint4 c = c4[i], m = m4[i];
-            bounds_acc(c.x, m.x, mc, mm, lc, lm);
-            bounds_acc(c.y, m.y, mc, mm, lc, lm);
-            bounds_acc(c.z, m.z, mc, mm, lc, lm);
-            bounds_acc(c.w, m.w, mc, mm, lc, lm);
-        }
-        head = n4 * 4;
-    }
-    for (size_t i = head + t; i < n; i += stride) bounds_acc(cpu[i], mem[i], mc, mm, lc, lm);
-    for (int o = 32; o > 0; o >>= 1) {
-        mc = max(mc, (uint32_t)__shfl_xor((int)mc, o));
-        mm = max(mm, (uint32_t)__shfl_xor((int)mm, o));
-        lc = min(lc, (uint32_t)__shfl_xor((int)lc, o));
-        lm = min(lm, (uint32_t)__shfl_xor((int)lm, o));
-    }
-    __shared__ uint32_t red[4][4];
-    const uint32_t w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[w][0] = mc; red[w][1] = mm; red[w][2] = lc; red[w][3] = lm; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (uint32_t q = 1; q < blockDim.x / 64; ++q) {
-            mc = max(mc, red[q][0]); mm = max(mm, red[q][1]); lc = min(lc, red[q][2]); lm = min(lm, red[q][3]);
-        }
-        atomicMax(&out[0], mc);
-        atomicMax(&out[1], mm);
-        atomicMin(&out[2], lc);
-        atomicMin(&out[3], lm);
-    }
-}
 
 // ---- dense value ranks (order-preserving key compression) ----
 constexpr uint32_t RANK_MAX_VALUE = 1u << 18;  // per dimension: 32 KB LDS bitmap
@@ -84,19 +41,23 @@ constexpr uint32_t RANK_WORDS = RANK_MAX_VALUE / 32;
 // Presence bitmaps of the cpu and mem values (value v -> bit v, v < 2^18), built in LDS
 // per block (test before set: after the first few elements almost every bit is already
 // there) and ORed into the global bitmaps, nonzero words only.  A value >= 2^18 sets
-// *over (the caller then falls back to raw-value keys and k_key_bounds).  The bounds
-// the placement needs (max, min positive) come out of the bitmaps (k_rank_tables), so
-// this one pass over cpu/mem replaces the bounds pass.
+// cnt[CN_OVER] (no dense ranks then: the LDS sort takes its generic fallback and the
+// thresholds are geometric).  The raw bounds come out of the same pass: cnt[CN_MAXC..CN_MINM]
+// (max cpu, max mem, smallest positive cpu, mem; the minima start at 0xFFFFFFFF).
+enum { CN_DC = 0, CN_DM = 1, CN_OVER = 6, CN_MAXC = 8, CN_MAXM = 9, CN_MINC = 10, CN_MINM = 11, CN_ELIG = 12,
+       CN_WORDS = 16 };
 __global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict__ cpu,
                                                       const uint32_t *__restrict__ mem, size_t n,
                                                       uint32_t *__restrict__ gbc, uint32_t *__restrict__ gbm,
-                                                      uint32_t *__restrict__ over) {
+                                                      uint32_t *__restrict__ cnt) {
     extern __shared__ uint32_t lbm[];  // [RANK_WORDS] cpu words, then [RANK_WORDS] mem words
     for (uint32_t i = threadIdx.x; i < 2 * RANK_WORDS; i += blockDim.x) lbm[i] = 0;
     __syncthreads();
     uint32_t *lc = lbm, *lm = lbm + RANK_WORDS;
     bool big = false;
+    uint32_t bxc = 0, bxm = 0, bnc = 0xFFFFFFFFu, bnm = 0xFFFFFFFFu;
     auto add = [&](uint32_t c, uint32_t m) {
+        bounds_acc(c, m, bxc, bxm, bnc, bnm);
         if ((c | m) >= RANK_MAX_VALUE) { big = true; return; }
         const uint32_t bc = 1u << (c & 31), bmk = 1u << (m & 31);
         if (!(lc[c >> 5] & bc)) atomicOr(&lc[c >> 5], bc);
@@ -125,7 +86,19 @@ __global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict
         head = n4 * 4;
     }
     for (size_t i = head + t; i < n; i += stride) add(cpu[i], mem[i]);
-    if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(over, 1u);
+    if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(&cnt[CN_OVER], 1u);
+    for (int o = 32; o > 0; o >>= 1) {
+        bxc = max(bxc, (uint32_t)__shfl_xor((int)bxc, o));
+        bxm = max(bxm, (uint32_t)__shfl_xor((int)bxm, o));
+        bnc = min(bnc, (uint32_t)__shfl_xor((int)bnc, o));
+        bnm = min(bnm, (uint32_t)__shfl_xor((int)bnm, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&cnt[CN_MAXC], bxc);
+        atomicMax(&cnt[CN_MAXM], bxm);
+        atomicMin(&cnt[CN_MINC], bnc);
+        atomicMin(&cnt[CN_MINM], bnm);
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < RANK_WORDS; i += blockDim.x) {
         if (lc[i]) atomicOr(&gbc[i], lc[i]);
@@ -202,12 +175,6 @@ __global__ void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__
     }
 }
 
-__global__ void k_iota_vals(size_t n, uint32_t C, uint32_t *__restrict__ vals) {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (size_t)gridDim.x * blockDim.x)
-        vals[i] = (uint32_t)(i % C);
-}
-
 __global__ void k_seg_offsets(uint32_t S, uint32_t C, uint32_t *__restrict__ off) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= S) off[i] = i * C;
@@ -278,12 +245,18 @@ static inline size_t ss_lds_bytes(uint32_t C) {
 }
 
 // u16 digit pair per container: hd | ld << 8 (dense ranks, ascending = descending demand)
+// The distinct counts, bounds and eligibility are device values (cnt, k_rank_tables /
+// k_thresholds): a batch the digits cannot express (cnt[CN_ELIG] = 0) leaves at once and
+// k_scen_sort takes its generic fallback.
 __global__ __launch_bounds__(256) void k_digits(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
-                                                size_t n, uint32_t dc, uint32_t dm, uint32_t wc, uint32_t wm,
+                                                size_t n, const uint32_t *__restrict__ cnt,
                                                 const uint32_t *__restrict__ bmc, const uint32_t *__restrict__ prc,
                                                 const uint32_t *__restrict__ bmm, const uint32_t *__restrict__ prm,
                                                 uint16_t *__restrict__ dig) {
     extern __shared__ uint32_t dgt[];  // [wc] bm, [wc] pre (cpu), [wm] bm, [wm] pre (mem) when they fit
+    if (!cnt[CN_ELIG]) return;
+    const uint32_t dc = cnt[CN_DC], dm = cnt[CN_DM];
+    const uint32_t wc = (cnt[CN_MAXC] >> 5) + 1u, wm = (cnt[CN_MAXM] >> 5) + 1u;
     const bool lds = wc + wm <= DG_TABLE_WORDS;
     if (lds) {
         for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) { dgt[i] = bmc[i]; dgt[wc + i] = prc[i]; }
@@ -316,11 +289,13 @@ __global__ __launch_bounds__(256) void k_digits(const uint32_t *__restrict__ cpu
 }
 
 struct ScenSortArgs {
-    uint32_t C, dc, dm, kpack;
+    uint32_t C, kpack;
+    const uint32_t *cnt;                     // distinct counts, bounds, eligibility (device, CN_*)
     const uint16_t *dig;                     // [S][C] k_digits
     const uint32_t *cval, *mval;             // ascending distinct values
+    const uint32_t *cpu, *mem;               // [S][C] the raw demands (the generic fallback)
     uint32_t *order, *s_cpu, *s_mem, *s_idx; // [S][C] FFD order, sorted cpu / mem / position word
-    uint32_t T[2 * FP_BUCKETS];              // bucket thresholds (cpu, then mem)
+    const uint32_t *T;                       // [2 FP_BUCKETS] bucket thresholds (cpu, then mem; device)
 };
 
 // the u16 digit rows are also counted, zeroed and scanned through 32/64-bit views: these
@@ -366,65 +341,10 @@ __device__ __forceinline__ void ss_row_scan(uint16_t *row, uint32_t lane, uint32
     reinterpret_cast<ss_u64a *>(row)[lane] = e0 | ((e0 + c0) << 16) | ((e0 + c0 + c1) << 32) | ((e0 + c0 + c1 + c2) << 48);
 }
 
-__global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char ssm[];
-    const uint32_t C = a.C, dc = a.dc, dm = a.dm;
-    uint16_t *X = reinterpret_cast<uint16_t *>(ssm);
-    uint8_t *LD = ssm + ss_align16((size_t)C * 2);
-    uint16_t *WH = reinterpret_cast<uint16_t *>(LD + ss_align16(C));     // [wave][digit]
-    uint32_t *HS = reinterpret_cast<uint32_t *>(WH + SS_WAVES * SS_DIG);  // bucket starts
-    uint32_t *HB = HS + SS_DIG;                                          // bucket ends
-    uint32_t *MV = HB + SS_DIG;                                          // mem value per ld
-    uint8_t *MB = reinterpret_cast<uint8_t *>(MV + SS_DIG);              // mem bucket per ld
-    uint8_t *CB = MB + SS_DIG;                                           // cpu bucket per hd
-    uint32_t *NEXT = reinterpret_cast<uint32_t *>(CB + SS_DIG);
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const size_t cb = (size_t)blockIdx.x * C;
-    const uint16_t *dig = a.dig + cb;
-    // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
-    const uint32_t hbits = dc > 1 ? 32u - (uint32_t)__builtin_clz(dc - 1u) : 0u;
-    const uint32_t lbits = dm > 1 ? 32u - (uint32_t)__builtin_clz(dm - 1u) : 0u;
-
-    for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
-    if (t < SS_DIG) {
-        const uint32_t mv = t < dm ? a.mval[dm - 1u - t] : 0u;
-        MV[t] = mv;
-        MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, mv) : 0;
-        CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, a.cval[dc - 1u - t]) : 0;
-    }
-    if (t == 0) NEXT[0] = 0u;
-    __syncthreads();
-
-    // A0: per-wave hd counts over the wave's slice [s0, s1), ld into LDS
-    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
-    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
-    uint16_t *myrow = WH + w * SS_DIG;
-    for (uint32_t p0 = s0; p0 < s1; p0 += 64 * SS_BATCH) {  // SS_BATCH loads in flight per lane
-        uint32_t dv[SS_BATCH];
-#pragma unroll
-        for (uint32_t k = 0; k < SS_BATCH; ++k) {
-            const uint32_t p = p0 + 64 * k + lane;
-            dv[k] = p < s1 ? (uint32_t)__builtin_nontemporal_load(&dig[p]) : 0u;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < SS_BATCH; ++k) {
-            const uint32_t p = p0 + 64 * k + lane;
-            if (p < s1) {
-                LD[p] = (uint8_t)(dv[k] >> 8);
-                ss_inc16(myrow, dv[k] & 0xFFu);
-            }
-        }
-    }
-    __syncthreads();
-#ifdef SS_STOP  // timing variants (tools/build_variant.sh): stop after phase N with an identity order
-    if (SS_STOP == 1) {
-        for (uint32_t i = t; i < C; i += blockDim.x) {
-            a.order[cb + i] = i; a.s_cpu[cb + i] = 1; a.s_mem[cb + i] = 1; a.s_idx[cb + i] = i;
-        }
-        return;
-    }
-#endif
+// exclusive (wave, digit) offsets of a pass in wave order from the per-wave counts in WH: bucket
+// starts in HS, ends in HB (the scheme of k_scen_sort's A0 -> A1)
+__device__ __forceinline__ void ss_offsets(uint16_t *WH, uint32_t *HS, uint32_t *HB, uint32_t t, uint32_t lane,
+                                           uint32_t w) {
     if (t < SS_DIG) {  // totals per digit (thread t = digit t)
         uint32_t s = 0;
 #pragma unroll
@@ -459,15 +379,121 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
         HB[t] = run;
     }
     __syncthreads();
+}
 
-#ifdef SS_STOP  // timing variants (tools/build_variant.sh): stop after phase N with an identity order
-    if (SS_STOP == 2) {
-        for (uint32_t i = t; i < C; i += blockDim.x) {
-            a.order[cb + i] = i; a.s_cpu[cb + i] = 1; a.s_mem[cb + i] = 1; a.s_idx[cb + i] = i;
+// The generic fallback of k_scen_sort (a batch without dense ranks: more than 256 distinct cpu or
+// mem values, or a value >= 2^18): the same (cpu desc, mem desc, index asc) order by a stable LSD
+// sort over the bytes of ~mem, then of ~cpu (ascending ~v = descending v), eight counting passes
+// with A0 / A1's per-wave scheme.  Pass k writes the order to X (LDS) when k is even and to this
+// scenario's `order` row when k is odd (pass 0 starts from the identity), so pass 7 leaves it in
+// `order`; a pass reads the row back through agent-scope loads (other waves of the workgroup wrote
+// it in the pass before).  Then the sorted fields as the fast path writes them.
+__device__ void ss_generic(const ScenSortArgs &a, uint16_t *X, uint16_t *WH, uint32_t *HS, uint32_t *HB,
+                           size_t cb, uint32_t C) {
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
+    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
+    uint16_t *myrow = WH + w * SS_DIG;
+    uint32_t *ord = a.order + cb;
+    const uint32_t *cpu = a.cpu + cb, *mem = a.mem + cb;
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t *key = k < 4 ? mem : cpu;
+        const uint32_t sh = 8u * (k & 3u);
+        auto src = [&](uint32_t p) -> uint32_t {
+            return k == 0 ? p
+                   : (k & 1u) ? (uint32_t)X[p]
+                              : __hip_atomic_load(&ord[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
+        __syncthreads();
+        for (uint32_t p = s0 + lane; p < s1; p += 64) ss_inc16(myrow, ((~key[src(p)]) >> sh) & 0xFFu);
+        __syncthreads();
+        ss_offsets(WH, HS, HB, t, lane, w);
+        for (uint32_t p0 = s0; p0 < s1; p0 += 64) {
+            const uint32_t p = p0 + lane;
+            const bool valid = p < s1;
+            const uint32_t j = valid ? src(p) : 0u;
+            const uint32_t d = valid ? ((~key[j]) >> sh) & 0xFFu : 0u;
+            const uint64_t m = ss_match(d, valid, 8);
+            const uint32_t off = myrow[d];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane's read before the update
+            if (valid) {
+                if ((m & lt) == 0) myrow[d] = (uint16_t)(off + __popcll(m));
+                const uint32_t q = off + (uint32_t)__popcll(m & lt);
+                if (k & 1u) ord[q] = j;
+                else X[q] = (uint16_t)j;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
+        __syncthreads();
+    }
+    for (uint32_t P = t; P < C; P += blockDim.x) {
+        const uint32_t j = __hip_atomic_load(&ord[P], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t cv = cpu[j], mv = mem[j];
+        a.s_cpu[cb + P] = cv;
+        a.s_mem[cb + P] = mv;
+        a.s_idx[cb + P] = P | (a.kpack ? (ss_bucket(a.T, cv) << 21) | (ss_bucket(a.T + FP_BUCKETS, mv) << 26) : 0u);
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char ssm[];
+    const uint32_t C = a.C, dc = a.cnt[CN_DC], dm = a.cnt[CN_DM];
+    uint16_t *X = reinterpret_cast<uint16_t *>(ssm);
+    uint8_t *LD = ssm + ss_align16((size_t)C * 2);
+    uint16_t *WH = reinterpret_cast<uint16_t *>(LD + ss_align16(C));     // [wave][digit]
+    uint32_t *HS = reinterpret_cast<uint32_t *>(WH + SS_WAVES * SS_DIG);  // bucket starts
+    uint32_t *HB = HS + SS_DIG;                                          // bucket ends
+    uint32_t *MV = HB + SS_DIG;                                          // mem value per ld
+    uint8_t *MB = reinterpret_cast<uint8_t *>(MV + SS_DIG);              // mem bucket per ld
+    uint8_t *CB = MB + SS_DIG;                                           // cpu bucket per hd
+    uint32_t *NEXT = reinterpret_cast<uint32_t *>(CB + SS_DIG);
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const size_t cb = (size_t)blockIdx.x * C;
+    const uint16_t *dig = a.dig + cb;
+    // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
+    const uint32_t hbits = dc > 1 ? 32u - (uint32_t)__builtin_clz(dc - 1u) : 0u;
+    const uint32_t lbits = dm > 1 ? 32u - (uint32_t)__builtin_clz(dm - 1u) : 0u;
+    if (!a.cnt[CN_ELIG]) {  // no dense ranks for this batch (device flag, k_thresholds)
+        ss_generic(a, X, WH, HS, HB, cb, C);
         return;
     }
-#endif
+
+    for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
+    if (t < SS_DIG) {
+        const uint32_t mv = t < dm ? a.mval[dm - 1u - t] : 0u;
+        MV[t] = mv;
+        MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, mv) : 0;
+        CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, a.cval[dc - 1u - t]) : 0;
+    }
+    if (t == 0) NEXT[0] = 0u;
+    __syncthreads();
+
+    // A0: per-wave hd counts over the wave's slice [s0, s1), ld into LDS
+    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
+    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
+    uint16_t *myrow = WH + w * SS_DIG;
+    for (uint32_t p0 = s0; p0 < s1; p0 += 64 * SS_BATCH) {  // SS_BATCH loads in flight per lane
+        uint32_t dv[SS_BATCH];
+#pragma unroll
+        for (uint32_t k = 0; k < SS_BATCH; ++k) {
+            const uint32_t p = p0 + 64 * k + lane;
+            dv[k] = p < s1 ? (uint32_t)__builtin_nontemporal_load(&dig[p]) : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SS_BATCH; ++k) {
+            const uint32_t p = p0 + 64 * k + lane;
+            if (p < s1) {
+                LD[p] = (uint8_t)(dv[k] >> 8);
+                ss_inc16(myrow, dv[k] & 0xFFu);
+            }
+        }
+    }
+    __syncthreads();
+    ss_offsets(WH, HS, HB, t, lane, w);
+
     // A1: stable scatter by hd, each wave over its own slice
     for (uint32_t p00 = s0; p00 < s1; p00 += 64 * SS_BATCH) {
         uint32_t dv[SS_BATCH];
@@ -493,14 +519,6 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     }
     __syncthreads();
 
-#ifdef SS_STOP  // timing variants (tools/build_variant.sh): stop after phase N with an identity order
-    if (SS_STOP == 3) {
-        for (uint32_t i = t; i < C; i += blockDim.x) {
-            a.order[cb + i] = i; a.s_cpu[cb + i] = 1; a.s_mem[cb + i] = 1; a.s_idx[cb + i] = i;
-        }
-        return;
-    }
-#endif
     // B: each hd bucket sorted by ld by one wave and written out
     while (true) {
         uint32_t d = 0;
@@ -575,11 +593,9 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     }
 }
 
-}  // namespace
-
 // T[0] = 0; T[1..31] spread evenly over the ascending distinct positive values v[0..d)
 // (every value is a threshold when there are at most 31)
-static void value_thresholds(const uint32_t *v, uint32_t d, uint32_t *T) {
+__device__ void value_thresholds(const uint32_t *v, uint32_t d, uint32_t *T) {
     while (d && v[0] == 0) { ++v; --d; }  // zero is T[0]
     T[0] = 0;
     for (int k = 1; k < FP_BUCKETS; ++k) {
@@ -589,6 +605,32 @@ static void value_thresholds(const uint32_t *v, uint32_t d, uint32_t *T) {
         T[k] = v[i];
     }
 }
+
+// The pipeline's bucket thresholds, thr[0, K) cpu and [K, 2K) mem (thread 0: cpu, 1: mem): spread
+// over the batch's distinct values when it has dense ranks -- every bucket then spans about D / 31
+// distinct values (config 4: 79 cpu and 256 mem values -> 2.5 and 8 per bucket; geometric steps
+// spanned 9 and 43 at the top of the range, where most demands lie, and loose buckets cost exact
+// checks that miss) -- else geometric from the smallest positive to the largest demand.  Also the
+// LDS sort's eligibility: dense ranks with at most 256 values per dimension.  Any ascending choice
+// with T[0] = 0 is exact: the thresholds only decide how tight the candidate masks are.
+__global__ void k_thresholds(uint32_t *__restrict__ cnt, const uint32_t *__restrict__ cval,
+                             const uint32_t *__restrict__ mval, uint32_t *__restrict__ thr) {
+    const uint32_t d = threadIdx.x;
+    if (d > 1) return;
+    const bool ranks = cnt[CN_OVER] == 0;
+    uint32_t T[FP_BUCKETS];
+    if (ranks) {
+        value_thresholds(d ? mval : cval, cnt[d ? CN_DM : CN_DC], T);
+    } else {
+        const uint32_t lo = cnt[d ? CN_MINM : CN_MINC], hi = cnt[d ? CN_MAXM : CN_MAXC];
+        fp_thresholds(lo == 0xFFFFFFFFu ? 1u : lo, hi, T);
+    }
+    for (int k = 0; k < FP_BUCKETS; ++k) thr[d * FP_BUCKETS + k] = T[k];
+    if (d == 0)
+        cnt[CN_ELIG] = ranks && cnt[CN_DC] >= 1 && cnt[CN_DM] >= 1 && cnt[CN_DC] <= SS_DIG && cnt[CN_DM] <= SS_DIG;
+}
+
+}  // namespace
 
 static inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;
@@ -601,19 +643,11 @@ static inline unsigned grid_for(size_t n, unsigned block) {
 static int place_ws_need(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, size_t *need, size_t *sort_tmp_out) {
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;
-    // device-wide sorts are sized for the widest key they may take (u64); the
-    // segmented fallback is used only when scenario + key bits exceed 64
+    // the radix path sorts full-width u64 keys: device-wide for one scenario, segmented for several
     size_t sort_tmp = 0, t = 0;
     FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
                                      (uint32_t *)nullptr, SC, 0, 64, st));
     sort_tmp = t;
-    FP_HIP(rocprim::radix_sort_pairs(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                     (uint32_t *)nullptr, SC, 0, 32, st));
-    sort_tmp = t > sort_tmp ? t : sort_tmp;
-    FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                               (uint32_t *)nullptr, (uint32_t *)nullptr, (unsigned)SC, S,
-                                               (uint32_t *)nullptr, (uint32_t *)nullptr, 0, 32, st));
-    sort_tmp = t > sort_tmp ? t : sort_tmp;
     FP_HIP(rocprim::segmented_radix_sort_pairs(nullptr, t, (uint64_t *)nullptr,
                                                (uint64_t *)nullptr, (uint32_t *)nullptr,
                                                (uint32_t *)nullptr, (unsigned)SC, S,
@@ -621,7 +655,7 @@ static int place_ws_need(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, size_t *
     sort_tmp = t > sort_tmp ? t : sort_tmp;
     const size_t pipe_ws = fp_pipe_ws_bytes(c, S, C, N);
     if (pipe_ws == 0) return FP_EOVERFLOW;
-    const size_t rank_ws = 2 * (2 * RANK_WORDS * 4 + RANK_MAX_VALUE * 4) + 2 * 256;
+    const size_t rank_ws = 2 * (2 * RANK_WORDS * 4 + RANK_MAX_VALUE * 4) + CN_WORDS * 4 + 2 * FP_BUCKETS * 4 + 3 * 256;
     *need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + pipe_ws + rank_ws + 16 * 256;
     *sort_tmp_out = sort_tmp;
     return FP_OK;
@@ -669,180 +703,84 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     uint32_t *vals_out = (uint32_t *)fp_ws_take(c, SC * 4);
     uint32_t *offs = (uint32_t *)fp_ws_take(c, (S + 1) * 4);
     void *tmp = fp_ws_take(c, sort_tmp + 16);
-    uint32_t *bounds = (uint32_t *)fp_ws_take(c, 16);
-    // rank tables: bitmaps + prefix counts [2][RANK_WORDS] each, value tables, counts
+    // rank tables: bitmaps + prefix counts [2][RANK_WORDS] each, value tables, counts / bounds /
+    // eligibility (CN_*), thresholds [2][FP_BUCKETS] -- all device-resident, nothing is read back
     uint32_t *rbm = (uint32_t *)fp_ws_take(c, 2 * RANK_WORDS * 4);
     uint32_t *rpre = (uint32_t *)fp_ws_take(c, 2 * RANK_WORDS * 4);
     uint32_t *rval = (uint32_t *)fp_ws_take(c, 2 * RANK_MAX_VALUE * 4);
-    uint32_t *rcnt = (uint32_t *)fp_ws_take(c, 32);
-    if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !bounds || !rbm || !rpre || !rval ||
-        !rcnt)
+    uint32_t *rcnt = (uint32_t *)fp_ws_take(c, CN_WORDS * 4);
+    uint32_t *thr = (uint32_t *)fp_ws_take(c, 2 * FP_BUCKETS * 4);
+    if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !rbm || !rpre || !rval || !rcnt || !thr)
         return FP_ENOMEM;
 
-    // ---- 1-3: FFD order ----
+    // ---- 1-2: values, dense ranks, bounds, thresholds, LDS-sort eligibility (device) ----
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_SORT, &ev);
-    // value bitmaps -> dense ranks, distinct counts and bounds in one pass (values < 2^18)
     FP_HIP(hipMemsetAsync(rbm, 0, 2 * RANK_WORDS * 4, st));
-    FP_HIP(hipMemsetAsync(rcnt, 0, 32, st));
+    FP_HIP(hipMemsetAsync(rcnt, 0, CN_WORDS * 4, st));
+    FP_HIP(hipMemsetAsync(rcnt + CN_MINC, 0xFF, 8, st));  // the minima start at 0xFFFFFFFF
     {
         unsigned gb = grid_for((SC + 3) / 4, 256);
         if (gb > 1024) gb = 1024;  // each block merges its bitmaps once
         FP_HIP(hipFuncSetAttribute((const void *)k_value_bitmap, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(2 * RANK_WORDS * 4)));
-        k_value_bitmap<<<gb, 256, 2 * RANK_WORDS * 4, st>>>(b->cpu_m, b->mem_mib, SC, rbm, rbm + RANK_WORDS, rcnt + 6);
+        k_value_bitmap<<<gb, 256, 2 * RANK_WORDS * 4, st>>>(b->cpu_m, b->mem_mib, SC, rbm, rbm + RANK_WORDS, rcnt);
         FP_HIP(hipGetLastError());
         k_rank_tables<<<2, 1024, 0, st>>>(rbm, rbm + RANK_WORDS, RANK_WORDS, RANK_WORDS, rpre, rpre + RANK_WORDS, rval,
                                           rval + RANK_MAX_VALUE, rcnt);
         FP_HIP(hipGetLastError());
-    }
-    FP_HIP(hipMemcpyAsync(c->h_small, rcnt, 28, hipMemcpyDeviceToHost, st));
-    FP_HIP(hipStreamSynchronize(st));
-    const uint32_t *hs = (const uint32_t *)c->h_small;
-    const bool ranks = hs[6] == 0;
-    uint32_t maxc = hs[2], maxm = hs[3], minc = hs[4], minm = hs[5];
-    const uint32_t dc = hs[0], dm = hs[1];
-    if (!ranks) {  // a value >= 2^18: raw-value keys, exact bounds
-        FP_HIP(hipMemsetAsync(bounds, 0, 8, st));
-        FP_HIP(hipMemsetAsync(bounds + 2, 0xFF, 8, st));
-        k_key_bounds<<<grid_for((SC + 3) / 4, 256) < 2048 ? grid_for((SC + 3) / 4, 256) : 2048, 256, 0, st>>>(
-            b->cpu_m, b->mem_mib, SC, bounds);
+        k_thresholds<<<1, 64, 0, st>>>(rcnt, rval, rval + RANK_MAX_VALUE, thr);
         FP_HIP(hipGetLastError());
-        FP_HIP(hipMemcpyAsync(c->h_small, bounds, 16, hipMemcpyDeviceToHost, st));
-        FP_HIP(hipStreamSynchronize(st));
-        maxc = hs[0]; maxm = hs[1]; minc = hs[2]; minm = hs[3];
     }
-    uint32_t cbits = fp_bitwidth(maxc), mbits = fp_bitwidth(maxm);
-    // dense ranks as key fields (a nonzero key only)
-    const uint32_t *bmc = nullptr, *bmm = nullptr, *prc = nullptr, *prm = nullptr;
-    const uint32_t *cval = nullptr, *mval = nullptr;
-    if (ranks && cbits + mbits > 0) {
-        if (dc == 0 || dm == 0) return FP_EDEVICE;  // SC > 0: at least one value each
-        bmc = rbm; bmm = rbm + RANK_WORDS; prc = rpre; prm = rpre + RANK_WORDS;
-        cval = rval; mval = rval + RANK_MAX_VALUE;
-        cbits = fp_bitwidth(dc - 1);
-        mbits = fp_bitwidth(dm - 1);
-    }
-    // Per-scenario LDS sort: dense ranks with at most 256 values per dimension and a
-    // scenario that fits LDS (C <= 51k).  FP_OPT_SCEN_SORT = 0 keeps the radix path.
-    const bool scen_sort = ranks && dc >= 1 && dm >= 1 && dc <= SS_DIG && dm <= SS_DIG &&
-                           ss_lds_bytes(C) <= SS_LDS_CAP &&
-                           fp_opt(c, FP_OPT_SCEN_SORT, 1) != 0;
-    if (scen_sort) {
-        uint32_t tc[FP_BUCKETS], tm[FP_BUCKETS];
-        {
-            std::vector<uint32_t> hv((size_t)dc + dm);
-            FP_HIP(hipMemcpyAsync(hv.data(), rval, (size_t)dc * 4, hipMemcpyDeviceToHost, st));
-            FP_HIP(hipMemcpyAsync(hv.data() + dc, rval + RANK_MAX_VALUE, (size_t)dm * 4, hipMemcpyDeviceToHost, st));
-            FP_HIP(hipStreamSynchronize(st));
-            value_thresholds(hv.data(), dc, tc);
-            value_thresholds(hv.data() + dc, dm, tm);
-        }
+    // ---- 3a: per-scenario LDS sort (scenarios of at most ~50k containers; host-known).  A batch
+    // without dense ranks of <= 256 values per dimension takes k_scen_sort's generic fallback,
+    // chosen on the device.  FP_OPT_SCEN_SORT = 0 keeps the radix path. ----
+    if (ss_lds_bytes(C) <= SS_LDS_CAP && fp_opt(c, FP_OPT_SCEN_SORT, 1) != 0) {
         uint16_t *dig = (uint16_t *)keys_in;  // SC x u16 digit pairs (keys_in holds SC x 8 B)
         {
-            const uint32_t wc = (maxc >> 5) + 1, wm = (maxm >> 5) + 1;
-            const size_t tl = wc + wm <= DG_TABLE_WORDS ? (size_t)(wc + wm) * 8 : 0;
+            const size_t tl = (size_t)DG_TABLE_WORDS * 8;  // rank tables staged when they fit (device choice)
             FP_HIP(hipFuncSetAttribute((const void *)k_digits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
             k_digits<<<grid_for((SC + 3) / 4, 256) < 4096 ? grid_for((SC + 3) / 4, 256) : 4096, 256, tl, st>>>(
-                b->cpu_m, b->mem_mib, SC, dc, dm, wc, wm, rbm, rpre, rbm + RANK_WORDS, rpre + RANK_WORDS, dig);
+                b->cpu_m, b->mem_mib, SC, rcnt, rbm, rpre, rbm + RANK_WORDS, rpre + RANK_WORDS, dig);
             FP_HIP(hipGetLastError());
         }
         ScenSortArgs sa;
-        sa.C = C; sa.dc = dc; sa.dm = dm; sa.kpack = fp_pipe_kpack(c, C);
+        sa.C = C; sa.kpack = fp_pipe_kpack(c, C);
+        sa.cnt = rcnt;
         sa.dig = dig;
         sa.cval = rval; sa.mval = rval + RANK_MAX_VALUE;
+        sa.cpu = b->cpu_m; sa.mem = b->mem_mib;
         fp_pipe_soa soa;
         if (int rs = fp_pipe_soa_take(c, SC, &soa)) return rs;
         sa.order = vals_out; sa.s_cpu = soa.s_cpu; sa.s_mem = soa.s_mem; sa.s_idx = soa.s_idx;
-        memcpy(sa.T, tc, sizeof(tc));
-        memcpy(sa.T + FP_BUCKETS, tm, sizeof(tm));
+        sa.T = thr;
         const size_t lds = ss_lds_bytes(C);
         FP_HIP(hipFuncSetAttribute((const void *)k_scen_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         k_scen_sort<<<S, 1024, lds, st>>>(sa);
         FP_HIP(hipGetLastError());
         fp_prof_end(c, FP_K_SORT, ev);
         return fp_pipe_launch(c, S, C, N, b->scen_base, vals_out, nullptr, 4, 0, 0, 0, rval, rval + RANK_MAX_VALUE, b,
-                              tc, tm, &soa);
+                              thr, &soa);
     }
-    const uint32_t kbits = cbits + mbits;
-    const uint64_t cmax = cbits ? ((cbits == 64 ? ~0ull : ((1ull << cbits) - 1))) : 0ull;
-    const uint64_t mmax = mbits ? ((1ull << mbits) - 1) : 0ull;
-    const uint32_t sbits = fp_bitwidth(S - 1);
-    const uint32_t *order = nullptr;
-    const void *skeys = nullptr;
-    uint32_t key_bytes = 8;
-    if (kbits == 0) {
-        k_iota_vals<<<grid_for(SC, 256), 256, 0, st>>>(SC, C, vals_out);
-        FP_HIP(hipGetLastError());
-        order = vals_out;
-    } else if (kbits <= 32 && S > 1 && fp_opt(c, FP_OPT_SEGSORT, 1) != 0) {
-        // many scenarios: per-scenario segments, so the key holds no scenario field (config 4:
-        // 15 bits of radix instead of 27; sort 7.3 -> 5.4 ms for 4096 x 50k)
-        uint32_t *k_in = (uint32_t *)keys_in, *k_out = (uint32_t *)keys_out;
-        k_make_keys<uint32_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, 64, mbits, cmax, mmax,
-                                                                 bmc, prc, bmm, prm, k_in, vals_in);
-        FP_HIP(hipGetLastError());
-        k_seg_offsets<<<(S + 1 + 255) / 256, 256, 0, st>>>(S, C, offs);
-        FP_HIP(hipGetLastError());
-        FP_HIP(rocprim::segmented_radix_sort_pairs(tmp, sort_tmp, k_in, k_out, vals_in, vals_out, (unsigned)SC, S,
-                                                   offs, offs + 1, 0, kbits, st));
-        order = vals_out;
-        skeys = k_out;
-        key_bytes = 4;
-    } else if (kbits + sbits <= 32) {
-        uint32_t *k_in = (uint32_t *)keys_in, *k_out = (uint32_t *)keys_out;
-        k_make_keys<uint32_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, kbits, mbits, cmax,
-                                                                 mmax, bmc, prc, bmm, prm, k_in, vals_in);
-        FP_HIP(hipGetLastError());
-        FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, k_in, k_out, vals_in, vals_out, SC, 0, kbits + sbits, st));
-        order = vals_out;
-        skeys = k_out;
-        key_bytes = 4;
-    } else if (kbits + sbits <= 64) {
-        k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, kbits, mbits, cmax,
-                                                                 mmax, bmc, prc, bmm, prm, keys_in, vals_in);
-        FP_HIP(hipGetLastError());
-        FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in, vals_out, SC, 0,
-                                         kbits + sbits, st));
-        order = vals_out;
-        skeys = keys_out;
+    // ---- 3b: radix path: key = (~cpu << 32 | ~mem), value = the container's index; a stable
+    // radix sort over all 64 bits gives (cpu desc, mem desc, index asc) without knowing the key
+    // range on the host (FP_OPT_SEGSORT no longer changes anything: several scenarios are always
+    // sorted as segments, one scenario device-wide) ----
+    const uint64_t full = 0xFFFFFFFFull;
+    k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, 64, 32, full, full, nullptr,
+                                                             nullptr, nullptr, nullptr, keys_in, vals_in);
+    FP_HIP(hipGetLastError());
+    if (S == 1) {
+        FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in, vals_out, SC, 0, 64, st));
     } else {
-        // full-width cpu and mem (64 key bits): per-scenario segments
-        k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, 64, mbits, cmax,
-                                                                 mmax, bmc, prc, bmm, prm, keys_in, vals_in);
-        FP_HIP(hipGetLastError());
         k_seg_offsets<<<(S + 1 + 255) / 256, 256, 0, st>>>(S, C, offs);
         FP_HIP(hipGetLastError());
-        FP_HIP(rocprim::segmented_radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in,
-                                                   vals_out, (unsigned)SC, S, offs, offs + 1, 0,
-                                                   kbits, st));
-        order = vals_out;
-        skeys = keys_out;
+        FP_HIP(rocprim::segmented_radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in, vals_out, (unsigned)SC,
+                                                   S, offs, offs + 1, 0, 64, st));
     }
     fp_prof_end(c, FP_K_SORT, ev);
-
-    // ---- bucket thresholds of the pipeline's candidate masks ----
-    // With dense ranks the batch's distinct demand values are known (cval/mval): the
-    // thresholds are spread evenly over them, so every bucket spans about D / 31 distinct
-    // values (config 4: 79 cpu and 256 mem values -> 2.5 and 8 per bucket).  Geometric
-    // steps from min to max spanned 9 and 43 values per bucket at the top of the range,
-    // where most demands lie, and the loose buckets cost exact checks that miss.
-    // Otherwise (values >= 2^18): geometric from the smallest positive to the largest demand.
-    uint32_t tc[FP_BUCKETS], tm[FP_BUCKETS];
-    if (cval) {
-        std::vector<uint32_t> hv((size_t)dc + dm);
-        FP_HIP(hipMemcpyAsync(hv.data(), cval, (size_t)dc * 4, hipMemcpyDeviceToHost, st));
-        FP_HIP(hipMemcpyAsync(hv.data() + dc, mval, (size_t)dm * 4, hipMemcpyDeviceToHost, st));
-        FP_HIP(hipStreamSynchronize(st));
-        value_thresholds(hv.data(), dc, tc);
-        value_thresholds(hv.data() + dc, dm, tm);
-    } else {
-        fp_thresholds(minc == 0xFFFFFFFFu ? 1u : minc, maxc, tc);
-        fp_thresholds(minm == 0xFFFFFFFFu ? 1u : minm, maxm, tm);
-    }
-
     // ---- 4-5: placement + cost ----
-    return fp_pipe_launch(c, S, C, N, b->scen_base, order, skeys, key_bytes, mbits, cmax, mmax, cval, mval, b, tc, tm,
+    return fp_pipe_launch(c, S, C, N, b->scen_base, vals_out, keys_out, 8, 32, full, full, nullptr, nullptr, b, thr,
                           nullptr);
 }
 

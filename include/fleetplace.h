@@ -23,13 +23,15 @@
  *   - fp_dev_* take DEVICE (HBM) pointers of the context's device and are
  *     asynchronous on the context's stream.  Kernel-side errors of fp_dev_* calls
  *     (FP_ECORRUPT input, FP_EDEVICE from the placement pipeline's deadlock guard) are
- *     sticky: the first one raised is kept until fp_ctx_sync() (or fp_dev_levelize's own
- *     mid-call check) reports it and clears it.  A host-pointer call reports only the
- *     errors of its own kernels (it has its own error word): a pending asynchronous error
- *     neither fails it nor is cleared by it.
- *     fp_dev_place_batch and fp_dev_levelize read a few words back to size their
- *     sort keys / level count, so they synchronise the stream once or twice per call;
- *     their kernels stay queued and asynchronous.
+ *     sticky: the first one raised is kept until fp_ctx_sync() reports it and clears it.
+ *     A host-pointer call reports only the errors of its own kernels (it has its own error
+ *     word): a pending asynchronous error neither fails it nor is cleared by it.
+ *     fp_dev_* calls read nothing back: every data-dependent choice (key range, sort path,
+ *     bucket thresholds, level count, a corrupt CSR) is made on the device, so a caller can
+ *     queue call i+1 behind call i's collectives without a host stall.  The exceptions: the
+ *     first call of a shape larger than any before it grows the context's workspace (one
+ *     stream synchronisation), and FP_OPT_LEVELIZE_SYNC = 1 (the level-synchronous
+ *     levelizer) reads its frontier size back once per 64 levels.
  *   - fp_ctx_set_stream first waits for the context's last fp_dev_* call (an event
  *     recorded on the old stream; the workspace is reused by every call).  It never
  *     touches the old stream handle itself, so a caller may destroy that stream once

@@ -34,20 +34,30 @@ def test_pipeline_deadlock_guard_is_reported_by_sync(planner, opts):
     torch.cuda.empty_cache()
 
 
-def test_dev_levelize_corrupt_csr_reported_once(planner):
+@pytest.mark.parametrize("bad", ["col", "row_ptr"])
+def test_dev_levelize_corrupt_csr_reported_once(bad, planner):
+    """fp_dev_levelize is asynchronous (no read-back inside): a corrupt CSR is found on the
+    device, every later kernel of the call does nothing, and fp_ctx_sync reports FP_ECORRUPT
+    exactly once.  A valid call afterwards, asynchronous too, is exact."""
     import torch
     from fleetflow_amd._lib import FP_ECORRUPT, FleetplaceError
     dev = "cuda:0"
-    rp = torch.tensor([0, 1, 2], dtype=torch.int32, device=dev)
-    col = torch.tensor([0, 7], dtype=torch.int32, device=dev)  # 7 >= V
+    rp = torch.tensor([0, 1, 2] if bad == "col" else [0, 2, 1], dtype=torch.int32, device=dev)
+    col = torch.tensor([0, 7] if bad == "col" else [1, 0], dtype=torch.int32, device=dev)  # 7 >= V
     hd = torch.tensor([0, 1], dtype=torch.uint8, device=dev)
     lv = torch.empty(2, dtype=torch.int32, device=dev)
     od = torch.empty(2, dtype=torch.int32, device=dev)
     nc = torch.empty(1, dtype=torch.int32, device=dev)
+    planner.dev_levelize(rp, col, hd, lv, od, nc)  # returns at once: the error is sticky
     with pytest.raises(FleetplaceError) as e:
-        planner.dev_levelize(rp, col, hd, lv, od, nc)
+        planner.sync()
     assert e.value.code == FP_ECORRUPT
-    planner.sync()  # the mid-call check reported and cleared it
+    planner.sync()  # reported once, then cleared
+    rp2 = torch.tensor([0, 1, 1], dtype=torch.int32, device=dev)
+    col2 = torch.tensor([1], dtype=torch.int32, device=dev)
+    planner.dev_levelize(rp2, col2, hd, lv, od, nc)
+    planner.sync()
+    assert lv.tolist() == [0, 1] and od.tolist() == [0, 1] and nc.item() == 0
     level, order, ncyc = planner.levelize([0, 1, 1], [1], [0, 1])
     assert level.tolist() == [0, 1] and order.tolist() == [0, 1] and ncyc == 0
 

@@ -621,3 +621,50 @@ def test_feasibility_batch_vs_oracle(S, C, N, planner, O):
         ef, ec, _ = O.feasibility(tuple(np.asarray(x)[:k] for x in cont), nodes, want_bitmap=False)
         assert np.array_equal(fh[s * C:s * C + k], ef), s
         assert np.array_equal(ch[s * C:s * C + k], ec), s
+
+
+def test_levelize_deep_chain_three_sort_passes(planner, O):
+    """A chain of 1,050,000 vertices: levels need 21 bits, so the start order takes three LSD
+    passes of the counting sort (the key range is read on the device only); side edges and a
+    3-cycle as above."""
+    rng = np.random.default_rng(21)
+    V, chain = 1_100_000, 1_050_000
+    edges = [(v, v + 1) for v in range(chain - 1)]
+    a, b = rng.integers(0, V, 20_000), rng.integers(0, V, 20_000)
+    edges += [(int(x), int(y)) for x, y in zip(a, b) if chain <= x < y]
+    edges += [(V - 3, V - 2), (V - 2, V - 1), (V - 1, V - 3)]
+    rp, col = _csr(V, edges)
+    hd = np.zeros(V, np.uint8)
+    hd[np.unique(col)] = 1
+    level, order, ncyc = planner.levelize(rp, col, hd)
+    el, eo, en = O.levelize(rp, col, hd)
+    assert int(el[el != 0xFFFFFFFF].max()) == chain - 1
+    assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
+@pytest.mark.parametrize("S,C,dv", [(3, 50_000, 300), (2, 20_000, 257), (4, 8_000, 256)])
+def test_scen_sort_generic_fallback(S, C, dv, planner, O):
+    """Scenarios that fit the per-scenario LDS sort but whose batch has more than 256 distinct cpu
+    values (dv > 256) take k_scen_sort's generic LSD fallback, chosen on the device (no read-back);
+    dv = 256 stays on the digit path.  Plans, reasons and costs must be the oracle's either way."""
+    rng = np.random.default_rng(C + dv)
+    N = 2_000
+    conts, nodes = [], []
+    vals = rng.choice(np.arange(100, 100 + 20 * dv, 20), dv, replace=False).astype(np.uint32)
+    for s in range(S):
+        c, n = O.gen_scenario(SEED + 61, s, C, N, 7)
+        c = [np.array(a, np.uint32) for a in c]
+        c[0] = vals[rng.integers(0, dv, C)]
+        c[0][:dv] = vals                               # every value present in every scenario
+        conts.append(c)
+        nodes.append(n)
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    assign, reason, cost, after = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
+                                                      [cat(nodes, i) for i in range(5)], scen_base=7)
+    for s in range(S):
+        ea, er, eafter, _ = O.place(conts[s], nodes[s])
+        assert np.array_equal(assign[s * C:(s + 1) * C], ea), s
+        assert np.array_equal(reason[s * C:(s + 1) * C], er), s
+        assert int(cost[s]) == O.cost(ea, N, 7 + s)
+        for i in (0, 1, 3):
+            assert np.array_equal(after[i][s * N:(s + 1) * N], eafter[i])
