@@ -259,7 +259,7 @@ __global__ void k_edge_hop(uint32_t E, const uint4 *__restrict__ rec, const uint
 __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
                                  const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t *__restrict__ level,
                                  uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
-                                 bool pk, const uint32_t *__restrict__ bad) {
+                                 bool pk, bool push_src, const uint32_t *__restrict__ bad) {
     if (*bad) return;
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = v < V;
@@ -272,7 +272,7 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
         state[v] = ((uint64_t)l0 << 32) | indeg[v];
         level[v] = src && deg == 0 ? l0 : FP_NONE;
     }
-    const bool push = src && deg != 0;
+    const bool push = push_src && src && deg != 0;  // else k_tree_relax expands the sources' trees
     const uint64_t m = __ballot(push);
     if (!m) return;
     const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(m);
@@ -283,6 +283,135 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
     if (push)
         Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
             ((uint64_t)(pk ? l0 << 8 : l0) << 32) | v;
+}
+
+// ---- in-tree pre-pass (pointer jumping) ---------------------------------------------------
+// A vertex with exactly one parent has level(parent) + 1, so following the only-parent edges up
+// from v reaches the root of v's in-tree, r(v) (a vertex with no parent or several), at distance
+// d(v), and level(v) = level(r(v)) + d(v).  Wyllie's pointer jumping finds (r, d) for every vertex
+// in ceil(log2 V) + 1 edge-free rounds.  Trees rooted at a SOURCE then have final levels at once
+// (level(r) = has_deps(r)), and every edge from them into a join (a vertex with several parents)
+// is relaxed by one vertex-parallel pass (k_tree_relax) -- config 5's 500-deep chains cost log2
+// rounds instead of 500 dependent hops in k_lvl_async.  The async kernel then starts from the
+// joins that pass made ready and walks only the trees rooted at joins; it never meets a
+// source-rooted vertex (such a vertex's only in-edge comes from its source-rooted parent).
+// Link word per vertex: low 32 bits = r, high = d | flags.  Every (r, d) a round reads is a true
+// (ancestor, distance) pair, so the rounds may update in place.  A vertex on (or below) a cycle of
+// only-parent edges never reaches a root: its distance doubles every round, and at >= V it is
+// marked LK_CYC (never final, as Kahn leaves it).
+constexpr uint32_t LK_TERM = 1u << 31, LK_SRC = 1u << 30, LK_CYC = 1u << 29, LK_DIST = LK_CYC - 1u;
+constexpr uint32_t kTreeRounds = 32;  // flag words (rounds <= bits(V) + 1 <= 31)
+
+__device__ __forceinline__ uint64_t lk_ld(const uint64_t *p) {
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lk_st(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// roots (in-degree != 1) link to themselves, terminal; an only-parent child links to its parent
+// at distance 1 (exactly one edge names it, so exactly one store)
+__global__ void k_tree_init(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t V,
+                            const uint32_t *__restrict__ indeg, uint64_t *__restrict__ link,
+                            const uint32_t *__restrict__ bad) {
+    if (*bad) return;
+    const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= V) return;
+    const uint32_t du = indeg[u];
+    if (du != 1u) link[u] = ((uint64_t)(LK_TERM | (du == 0u ? LK_SRC : 0u)) << 32) | u;
+    const uint32_t e1 = row_ptr[u + 1];
+    for (uint32_t e = row_ptr[u]; e < e1; ++e) {
+        const uint32_t w = col[e];
+        if (indeg[w] == 1u) link[w] = (1ull << 32) | u;
+    }
+}
+
+// one jumping round: (r, d) <- (r(r), d + d(r)); round k > 0 runs only if round k - 1 left a
+// vertex unresolved (flags[k - 1]), so the host enqueues every round V could need and reads nothing
+__global__ void k_tree_jump(uint64_t *__restrict__ link, uint32_t V, uint32_t k, uint32_t *__restrict__ flags,
+                            const uint32_t *__restrict__ bad) {
+    if (*bad || (k && !flags[k - 1])) return;
+    const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool open = false;
+    if (u < V) {
+        uint64_t x = lk_ld(&link[u]);
+        if (!((x >> 32) & LK_TERM)) {
+            const uint64_t y = lk_ld(&link[(uint32_t)x]);
+            const uint32_t hy = (uint32_t)(y >> 32);
+            const uint32_t d = ((uint32_t)(x >> 32) & LK_DIST) + (hy & LK_DIST);
+            if ((hy & LK_CYC) || d >= V) x = (uint64_t)(LK_TERM | LK_CYC) << 32;
+            else x = ((uint64_t)((hy & (LK_TERM | LK_SRC)) | d) << 32) | (uint32_t)y;
+            lk_st(&link[u], x);
+            open = !((x >> 32) & LK_TERM);
+        }
+    }
+    if (__ballot(open) && (threadIdx.x & 63) == 0) atomicOr(&flags[k], 1u);
+}
+
+// Source-rooted vertices get their final level; their edges into joins are relaxed (the packed
+// state words of k_lvl_async: level max, parents - 1), and a join whose last parent this was goes
+// to the queues.  A join may also finish inside k_lvl_async: each edge is relaxed exactly once,
+// here (source-rooted parent) or there.
+__global__ void k_tree_relax(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
+                             const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
+                             const uint64_t *__restrict__ link, uint32_t V, uint32_t *__restrict__ level,
+                             uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
+                             bool pk, const uint32_t *__restrict__ bad) {
+    if (*bad) return;
+    const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t lvl = 0, e = 0, e1 = 0;
+    bool fin = false;
+    if (u < V) {
+        const uint64_t x = link[u];
+        const uint32_t hx = (uint32_t)(x >> 32);
+        if ((hx & (LK_SRC | LK_CYC)) == LK_SRC) {
+            fin = true;
+            lvl = (hd[(uint32_t)x] ? 1u : 0u) + (hx & LK_DIST);
+            level[u] = lvl;
+            e = row_ptr[u];
+            e1 = row_ptr[u + 1];
+        }
+    }
+    uint32_t my_max = lvl;
+    for (int o = 32; o > 0; o >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor((int)my_max, o));
+    if (lane == 0 && my_max) atomicMax(&ctl[26 * kCtlStride], my_max);
+    const uint32_t sh = (uint32_t)((u >> 6) % kShards);
+    // one edge per lane and step, the wave's ready joins pushed together
+    while (__ballot(fin && e < e1)) {
+        bool rdy = false;
+        uint32_t w = 0, wl = 0;
+        if (fin && e < e1) {
+            w = col[e++];
+            if (indeg[w] != 1u) {
+                uint64_t exp = (1ull << 32) | 2ull, cur = 0;
+                while (true) {
+                    const uint32_t nl = max((uint32_t)(exp >> 32), lvl + 1u);
+                    const uint64_t nv = ((uint64_t)nl << 32) | (uint32_t)((uint32_t)exp - 1u);
+                    uint64_t obs = exp;
+                    if (__hip_atomic_compare_exchange_strong(&state[w], &obs, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT)) {
+                        cur = nv;
+                        break;
+                    }
+                    exp = obs;
+                }
+                rdy = (uint32_t)cur == 0u;
+                wl = (uint32_t)(cur >> 32);
+            }
+        }
+        const uint64_t m = __ballot(rdy);
+        if (m) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&ctl[(kShards + sh) * kCtlStride], (uint32_t)__popcll(m));
+            base = __shfl(base, (int)leader);
+            if (rdy)
+                __hip_atomic_store(&Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))],
+                                   ((uint64_t)(pk ? wl << 8 : wl) << 32) | w, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
@@ -834,7 +963,11 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     // counting sort (FP_OPT_LEVEL_SORT, on by default) its histograms
     const bool level_sync = fp_opt(c, FP_OPT_LEVELIZE_SYNC, 0) != 0;
     const bool counting = fp_opt(c, FP_OPT_LEVEL_SORT, 1) != 0;
-    const size_t async_ws = level_sync ? 0 : (size_t)V * 8 * (1 + kShards) + (size_t)E * 16 * kHops + kCtlWords * 4;
+    // FP_OPT_TREE_JUMP (on by default): the in-tree pre-pass before k_lvl_async
+    const bool tree = !level_sync && E && fp_opt(c, FP_OPT_TREE_JUMP, 1) != 0;
+    const size_t async_ws = level_sync ? 0
+                                       : (size_t)V * 8 * (1 + kShards) + (size_t)E * 16 * kHops + kCtlWords * 4 +
+                                             (tree ? (size_t)V * 8 + kTreeRounds * 4 + 256 : 0);
     const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 : 0;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + async_ws + cs_ws + 23 * 256);
     if (rc) return rc;
@@ -875,14 +1008,30 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
         uint4 *erec = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
         uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16 * (kHops - 1)) : nullptr;
-        if (!state || !Q || !actl || (E && (!erec || !erec2))) return FP_ENOMEM;
+        uint64_t *link = tree ? (uint64_t *)fp_ws_take(c, (size_t)V * 8) : nullptr;
+        uint32_t *tflags = tree ? (uint32_t *)fp_ws_take(c, kTreeRounds * 4) : nullptr;
+        if (!state || !Q || !actl || (E && (!erec || !erec2)) || (tree && (!link || !tflags))) return FP_ENOMEM;
         FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
         FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
         // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
         const bool pk = V < (1u << 24);
         k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl,
-                                                             pk, bad);
+                                                             pk, !tree, bad);
         FP_HIP(hipGetLastError());
+        if (tree) {
+            FP_HIP(hipMemsetAsync(tflags, 0, kTreeRounds * 4, st));
+            k_tree_init<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, g->col, V, indeg, link, bad);
+            FP_HIP(hipGetLastError());
+            // every non-terminal distance doubles per round: after bits(V) + 1 rounds it is >= V
+            const uint32_t rounds = fp_bitwidth((uint64_t)V) + 1u;
+            for (uint32_t k = 0; k < rounds; ++k) {
+                k_tree_jump<<<blocks_for(V, 256), 256, 0, st>>>(link, V, k, tflags, bad);
+                FP_HIP(hipGetLastError());
+            }
+            k_tree_relax<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, g->col, g->has_deps, indeg, link, V, level,
+                                                             state, Q, actl, pk, bad);
+            FP_HIP(hipGetLastError());
+        }
         if (E) {
             const unsigned eg = blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192;
             k_edge_rec<<<eg, 256, 0, st>>>(g->row_ptr, g->col, E, V, indeg, erec, bad);

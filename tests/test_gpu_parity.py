@@ -66,8 +66,9 @@ def _csr(V, edges):
     return rp, col
 
 
+@pytest.mark.parametrize("tree", [1, 0])
 @pytest.mark.parametrize("shape", ["star", "dup_and_self", "long_chain_fanout", "wide_hubs"])
-def test_levelize_async_shapes(shape, planner, O):
+def test_levelize_async_shapes(shape, tree, planner, O):
     """Shapes aimed at the asynchronous levelizer's paths: wave-cooperative expansion
     (a vertex with thousands of dependents), duplicate edges and self loops (CAS
     retries, CYCLE), chain continuation with fan-out side edges, many hubs."""
@@ -92,7 +93,52 @@ def test_levelize_async_shapes(shape, planner, O):
     hd = np.zeros(V, np.uint8)
     hd[np.unique(col)] = 1
     hd[rng.integers(0, V, V // 10)] = 1  # deps outside the target set
-    level, order, ncyc = planner.levelize(rp, col, hd)
+    planner.set_option("tree_jump", tree)
+    try:
+        level, order, ncyc = planner.levelize(rp, col, hd)
+    finally:
+        planner.set_option("tree_jump")
+    el, eo, en = O.levelize(rp, col, hd)
+    assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
+@pytest.mark.parametrize("tree", [1, 0])
+@pytest.mark.parametrize("shape", ["ring_with_tails", "join_then_chain", "random_forest", "cycle_fed_tree"])
+def test_levelize_tree_shapes(shape, tree, planner, O):
+    """The in-tree pre-pass (fp_order.hip k_tree_*): rings of only-parent edges with chains
+    hanging off them (never final: LK_CYC), a deep chain below a join (walked by k_lvl_async,
+    not pre-resolved), a 200k-vertex random forest (every vertex source-rooted, depth ~ hundreds),
+    and a tree fed by a cycle member; pre-pass on and off give the oracle's levels and order."""
+    rng = np.random.default_rng(11)
+    if shape == "ring_with_tails":
+        V = 20_000
+        edges = [(v, (v + 1) % 1000) for v in range(1000)]            # a 1000-ring, in-degree 1 each
+        edges += [(int(a), int(b)) for a, b in zip(rng.integers(0, 1000, 300), range(1000, 1300))]
+        edges += [(v, v + 1) for v in range(1300, 5000)]              # a chain from a source
+        edges += [(int(a), int(b)) for a, b in zip(rng.integers(1000, 5000, 8000), rng.integers(5000, V, 8000))]
+    elif shape == "join_then_chain":
+        V = 12_000
+        edges = [(0, 2), (1, 2)] + [(v, v + 1) for v in range(2, 6000)]
+        edges += [(int(a), int(b)) for a, b in zip(rng.integers(2, 6000, 9000), rng.integers(6000, V, 9000))]
+    elif shape == "random_forest":
+        V = 200_000
+        par = (rng.random(V - 1) * np.arange(1, V)).astype(np.int64)  # parent < child: a forest
+        edges = list(zip(par.tolist(), range(1, V)))
+        edges += [(int(a), int(b)) for a, b in zip(rng.integers(0, V // 2, 2000), rng.integers(V // 2, V, 2000)) if a < b]
+    else:
+        V = 9_000
+        edges = [(0, 1), (1, 2), (2, 0), (3, 0)]                      # 0 has two parents (3 and 2)
+        edges += [(2, 4)] + [(v, v + 1) for v in range(4, 4000)]      # below the cycle: never final
+        edges += [(5000 + i, 5001 + i) for i in range(3000)] + [(7000, 300), (8500, 8600)]
+    rp, col = _csr(V, edges)
+    hd = np.zeros(V, np.uint8)
+    hd[np.unique(col)] = 1
+    hd[rng.integers(0, V, V // 7)] = 1
+    planner.set_option("tree_jump", tree)
+    try:
+        level, order, ncyc = planner.levelize(rp, col, hd)
+    finally:
+        planner.set_option("tree_jump")
     el, eo, en = O.levelize(rp, col, hd)
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
@@ -142,10 +188,15 @@ def test_levelize_async_unpacked_entries(planner, O):
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
-def test_levelize_config5_full_size(planner, O):
+@pytest.mark.parametrize("tree", [1, 0])
+def test_levelize_config5_full_size(tree, planner, O):
     """BASELINE config 5: 1M vertices (1000 chains x 500 + 50 layers x 10k), 333 3-cycles."""
     rp, col, hd = O.gen_dag(SEED + 5, 1000, 500, 50, 10_000, 333)
-    level, order, ncyc = planner.levelize(rp, col, hd)
+    planner.set_option("tree_jump", tree)
+    try:
+        level, order, ncyc = planner.levelize(rp, col, hd)
+    finally:
+        planner.set_option("tree_jump")
     el, eo, en = O.levelize(rp, col, hd)
     assert ncyc == en == 999
     assert np.array_equal(level, el) and np.array_equal(order, eo)
