@@ -232,7 +232,7 @@ __global__ void k_argmin_cost(const uint64_t *__restrict__ cost, uint32_t n, uin
 // LDS: X u16[C] + ld u8[C] + [16][256] u16 + tables (~11.5 KB) -> C <= ~50.7k.
 constexpr uint32_t SS_DIG = 256;     // digits per dimension (dense ranks)
 constexpr uint32_t SS_WAVES = 16;
-constexpr uint32_t SS_BATCH = 8;     // digit loads in flight per lane in A0 / A1
+constexpr uint32_t SS_CHUNKS = 50;   // 64-container chunks per wave slice: C <= 16 x 50 x 64 = 51,200
 constexpr uint32_t SS_REG = 16;      // B: buckets of up to 64 x SS_REG containers are reordered in registers
 constexpr size_t SS_LDS_CAP = 160 * 1024;
 constexpr uint32_t DG_TABLE_WORDS = 4096;  // k_digits stages rank tables of at most this many words in LDS
@@ -437,6 +437,16 @@ __device__ void ss_generic(const ScenSortArgs &a, uint16_t *X, uint16_t *WH, uin
     }
 }
 
+#ifdef FP_PIPE_STATS
+// diagnostics build: k_scen_sort phase cycles summed over workgroups (fp_debug_sort_stats):
+// [0] A0 [1] offsets [2] A1 [3] B (until the last wave) [4] B busy summed over waves [5] workgroups
+// [6] largest bucket [7] whole kernel
+__device__ unsigned long long g_sort_stats[8];
+#define SS_CLK() __builtin_amdgcn_s_memtime()
+#else
+#define SS_CLK() 0ull
+#endif
+
 __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char ssm[];
     const uint32_t C = a.C, dc = a.cnt[CN_DC], dm = a.cnt[CN_DM];
@@ -469,46 +479,43 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
         CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, a.cval[dc - 1u - t]) : 0;
     }
     if (t == 0) NEXT[0] = 0u;
+    const unsigned long long ck0 = SS_CLK();
     __syncthreads();
 
     // A0: per-wave hd counts over the wave's slice [s0, s1), ld into LDS
     const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
     const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
     uint16_t *myrow = WH + w * SS_DIG;
-    for (uint32_t p0 = s0; p0 < s1; p0 += 64 * SS_BATCH) {  // SS_BATCH loads in flight per lane
-        uint32_t dv[SS_BATCH];
+    // the wave's whole slice (<= SS_CHUNKS x 64 digit pairs) is loaded at once and kept in
+    // registers for A1: one round trip instead of one per 8 chunks (round 3), and no second read
+    uint32_t dv[SS_CHUNKS];
 #pragma unroll
-        for (uint32_t k = 0; k < SS_BATCH; ++k) {
-            const uint32_t p = p0 + 64 * k + lane;
-            dv[k] = p < s1 ? (uint32_t)__builtin_nontemporal_load(&dig[p]) : 0u;
-        }
+    for (uint32_t k = 0; k < SS_CHUNKS; ++k) {
+        const uint32_t p = s0 + 64 * k + lane;
+        dv[k] = p < s1 ? (uint32_t)__builtin_nontemporal_load(&dig[p]) : 0u;
+    }
 #pragma unroll
-        for (uint32_t k = 0; k < SS_BATCH; ++k) {
-            const uint32_t p = p0 + 64 * k + lane;
-            if (p < s1) {
-                LD[p] = (uint8_t)(dv[k] >> 8);
-                ss_inc16(myrow, dv[k] & 0xFFu);
-            }
+    for (uint32_t k = 0; k < SS_CHUNKS; ++k) {
+        const uint32_t p = s0 + 64 * k + lane;
+        if (p < s1) {
+            LD[p] = (uint8_t)(dv[k] >> 8);
+            ss_inc16(myrow, dv[k] & 0xFFu);
         }
     }
     __syncthreads();
+    const unsigned long long ck1 = SS_CLK();
     ss_offsets(WH, HS, HB, t, lane, w);
+    const unsigned long long ck2 = SS_CLK();
 
-    // A1: stable scatter by hd, each wave over its own slice
-    for (uint32_t p00 = s0; p00 < s1; p00 += 64 * SS_BATCH) {
-        uint32_t dv[SS_BATCH];
+    // A1: stable scatter by hd, each wave over its own slice (digits from A0's registers)
+    {
 #pragma unroll
-        for (uint32_t k = 0; k < SS_BATCH; ++k) {
-            const uint32_t p = p00 + 64 * k + lane;
-            dv[k] = p < s1 ? (uint32_t)dig[p] & 0xFFu : 0u;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < SS_BATCH; ++k) {
-            const uint32_t p0 = p00 + 64 * k;
+        for (uint32_t k = 0; k < SS_CHUNKS; ++k) {
+            const uint32_t p0 = s0 + 64 * k;
             if (p0 >= s1) break;  // wave-uniform
             const uint32_t p = p0 + lane;
             const bool valid = p < s1;
-            const uint32_t d = dv[k];
+            const uint32_t d = dv[k] & 0xFFu;
             const uint64_t m = ss_match(d, valid, hbits);
             const uint32_t off = myrow[d];
             if (valid) {
@@ -518,6 +525,8 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
         }
     }
     __syncthreads();
+    const unsigned long long ck3 = SS_CLK();
+    uint32_t big = 0;
 
     // B: each hd bucket sorted by ld by one wave and written out
     while (true) {
@@ -527,6 +536,7 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
         if (d >= dc) break;
         const uint32_t lo = HS[d], hi = HB[d];
         if (lo == hi) continue;
+        big = max(big, hi - lo);
         // the row is zeroed, counted with atomics, scanned and consumed by the same wave: the
         // fences keep those accesses in order (s_waitcnt lgkmcnt(0), no compiler reordering)
         reinterpret_cast<ss_u64a *>(myrow)[lane] = 0ull;  // 4 digits per lane
@@ -591,6 +601,25 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
+#ifdef FP_PIPE_STATS
+    const unsigned long long ck4 = SS_CLK();
+    if (lane == 0) {
+        atomicAdd(&g_sort_stats[4], ck4 - ck3);
+        atomicMax(&g_sort_stats[6], (unsigned long long)big);
+    }
+    __syncthreads();
+    if (t == 0) {
+        const unsigned long long ck5 = SS_CLK();
+        atomicAdd(&g_sort_stats[0], ck1 - ck0);
+        atomicAdd(&g_sort_stats[1], ck2 - ck1);
+        atomicAdd(&g_sort_stats[2], ck3 - ck2);
+        atomicAdd(&g_sort_stats[3], ck5 - ck3);
+        atomicAdd(&g_sort_stats[5], 1ull);
+        atomicAdd(&g_sort_stats[7], ck5 - ck0);
+    }
+#else
+    (void)ck0; (void)ck1; (void)ck2; (void)ck3; (void)big;
+#endif
 }
 
 // T[0] = 0; T[1..31] spread evenly over the ascending distinct positive values v[0..d)
@@ -631,6 +660,18 @@ __global__ void k_thresholds(uint32_t *__restrict__ cnt, const uint32_t *__restr
 }
 
 }  // namespace
+
+#ifdef FP_PIPE_STATS
+extern "C" int fp_debug_sort_stats(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+        return FP_EDEVICE;
+    if (reset) {
+        static const unsigned long long zero[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sort_stats), zero, sizeof(zero)) != hipSuccess) return FP_EDEVICE;
+    }
+    return FP_OK;
+}
+#endif
 
 static inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;
@@ -735,7 +776,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     // ---- 3a: per-scenario LDS sort (scenarios of at most ~50k containers; host-known).  A batch
     // without dense ranks of <= 256 values per dimension takes k_scen_sort's generic fallback,
     // chosen on the device.  FP_OPT_SCEN_SORT = 0 keeps the radix path. ----
-    if (ss_lds_bytes(C) <= SS_LDS_CAP && fp_opt(c, FP_OPT_SCEN_SORT, 1) != 0) {
+    if (ss_lds_bytes(C) <= SS_LDS_CAP && C <= SS_WAVES * SS_CHUNKS * 64 && fp_opt(c, FP_OPT_SCEN_SORT, 1) != 0) {
         uint16_t *dig = (uint16_t *)keys_in;  // SC x u16 digit pairs (keys_in holds SC x 8 B)
         {
             const size_t tl = (size_t)DG_TABLE_WORDS * 8;  // rank tables staged when they fit (device choice)
