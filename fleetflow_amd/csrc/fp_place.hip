@@ -4,14 +4,15 @@
 // Pipeline per fp_dev_place_batch call -- asynchronous: every data-dependent choice (dense ranks,
 // the LDS sort's eligibility, the key range, the bucket thresholds) is made on the device, so the
 // host enqueues the whole call without reading anything back.
-//   1. k_value_bitmap + k_rank_tables: the distinct cpu and mem values of the batch (values below
-//      2^18) as presence bitmaps -> dense ranks and ascending value tables; the raw bounds (max,
-//      smallest positive) in the same pass
+//   1. k_value_bitmap + k_rank_tables: the distinct cpu and mem values of a sample (the first
+//      THR_SAMPLE scenarios; values below 2^18) as presence bitmaps -> ascending value tables; the
+//      raw bounds (max, smallest positive) in the same pass
 //   2. k_thresholds: the pipeline's bucket thresholds (spread over the distinct values, or
-//      geometric between the bounds) and the LDS sort's eligibility flag, into device memory
+//      geometric between the bounds), into device memory
 //   3a. scenarios of at most ~50k containers (host-known): the per-scenario LDS sort below
-//      (k_digits + k_scen_sort), which falls back, in the same kernel, to a generic stable LSD
-//      sort of the raw values when the batch has more than 256 distinct values or values >= 2^18
+//      (k_scen_sort: the scenario's own dense ranks), which falls back, in the same workgroup, to a
+//      generic stable LSD sort of the raw values when the scenario has more than 256 distinct
+//      values or values >= 2^18
 //   3b. larger scenarios: k_make_keys (full-width key (~cpu << 32 | ~mem), value = index) and a
 //      stable rocprim radix sort over 64 bits, segmented per scenario when there are several
 //   4. k_ffd_pipe   : (fp_pipe.hip) per scenario, containers in key order stream
@@ -41,11 +42,9 @@ constexpr uint32_t RANK_WORDS = RANK_MAX_VALUE / 32;
 // Presence bitmaps of the cpu and mem values (value v -> bit v, v < 2^18), built in LDS
 // per block (test before set: after the first few elements almost every bit is already
 // there) and ORed into the global bitmaps, nonzero words only.  A value >= 2^18 sets
-// cnt[CN_OVER] (no dense ranks then: the LDS sort takes its generic fallback and the
-// thresholds are geometric).  The raw bounds come out of the same pass: cnt[CN_MAXC..CN_MINM]
+// cnt[CN_OVER] (the thresholds are then geometric).  The raw bounds come out of the same pass: cnt[CN_MAXC..CN_MINM]
 // (max cpu, max mem, smallest positive cpu, mem; the minima start at 0xFFFFFFFF).
-enum { CN_DC = 0, CN_DM = 1, CN_OVER = 6, CN_MAXC = 8, CN_MAXM = 9, CN_MINC = 10, CN_MINM = 11, CN_ELIG = 12,
-       CN_WORDS = 16 };
+enum { CN_DC = 0, CN_DM = 1, CN_OVER = 6, CN_MAXC = 8, CN_MAXM = 9, CN_MINC = 10, CN_MINM = 11, CN_WORDS = 16 };
 __global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict__ cpu,
                                                       const uint32_t *__restrict__ mem, size_t n,
                                                       uint32_t *__restrict__ gbc, uint32_t *__restrict__ gbm,
@@ -147,30 +146,14 @@ __global__ __launch_bounds__(1024) void k_rank_tables(const uint32_t *__restrict
     }
 }
 
-__device__ __forceinline__ uint32_t rank_of(uint32_t v, const uint32_t *__restrict__ bm,
-                                            const uint32_t *__restrict__ pre) {
-    const uint32_t w = v >> 5;
-    return pre[w] + (uint32_t)__popc(bm[w] & ((1u << (v & 31)) - 1u));
-}
-
-// Key fields are (mask - c) and (mask - m) for descending order, c/m the values (tables
-// null) or their dense ranks.
-template <class KeyT>
-__global__ void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
-                            size_t n, uint32_t C, uint32_t kb, uint32_t mb, uint64_t cmax, uint64_t mmax,
-                            const uint32_t *__restrict__ bmc, const uint32_t *__restrict__ prec,
-                            const uint32_t *__restrict__ bmm, const uint32_t *__restrict__ prem,
-                            KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
+// Radix-path keys: (~cpu << 32) | ~mem (descending demands sort ascending), value = the index in
+// the scenario.
+__global__ void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem, size_t n, uint32_t C,
+                            uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = (uint32_t)i / C, j = (uint32_t)i - s * C;  // n = S * C < 2^32
-        const uint64_t sk = kb >= 64 ? 0ull : ((uint64_t)s << kb);
-        uint32_t c = cpu[i], m = mem[i];
-        if (bmc) {
-            c = rank_of(c, bmc, prec);
-            m = rank_of(m, bmm, prem);
-        }
-        keys[i] = (KeyT)(sk | ((cmax - c) << mb) | (mmax - m));
+        keys[i] = ((uint64_t)~cpu[i] << 32) | (uint32_t)~mem[i];
         vals[i] = j;
     }
 }
@@ -215,85 +198,47 @@ __global__ void k_argmin_cost(const uint64_t *__restrict__ cost, uint32_t n, uin
 //
 // Every scenario is sorted into FFD order (cpu desc, mem desc, index asc) by one workgroup
 // of 1024 threads in LDS.  It writes the order and the sorted cpu / mem / position words
-// itself, so no radix keys, onesweep passes or key decode touch HBM.  The digits are dense
-// value ranks, flipped so that an ascending digit means a descending demand:
-// hd = dc-1-rank(cpu), ld = dm-1-rank(mem), each below 256.
-//   k_digits   streaming pass at full occupancy (rank tables staged in LDS): one u16
-//              digit pair per container (hd | ld << 8)
-//   k_scen_sort, one workgroup per scenario:
-//     A0  wave w counts the hd digits of its contiguous slice of the scenario (packed u16
-//         LDS atomics) and keeps ld[j] in LDS; one scan gives every (wave, digit) its offset
-//     A1  each wave walks its slice in order, 64 containers at a time; a container's place
-//         among equal digits in the 64 is a match mask of ballots, so X[p] = index in
-//         stable hd order with no barrier inside the pass
-//     B   every hd bucket (~630 containers in config 4) is sorted by ld by one wave, stable
-//         the same way, and written straight to its final positions; the bucket's window of
-//         each output array is a few KB, so its scattered dword stores merge in L2
-// LDS: X u16[C] + ld u8[C] + [16][256] u16 + tables (~11.5 KB) -> C <= ~50.7k.
+// itself, so no radix keys, onesweep passes or key decode touch HBM.  The digits are the
+// scenario's own dense value ranks, flipped so that an ascending digit means a descending demand:
+// hd = dc-1-rank(cpu), ld = dm-1-rank(mem), each below 256.  k_scen_sort, one workgroup per
+// scenario:
+//   R   presence bitmaps of the scenario's cpu and mem values (v < 2^18) in LDS, their prefix
+//       popcounts and the value of every rank: dc, dm and the eligibility of the digit sort
+//       (<= 256 values per dimension) are the scenario's own, decided in the workgroup
+//   A0  each wave loads its contiguous slice of the scenario, ranks it into digit pairs (kept in
+//       registers), keeps ld[j] in LDS and counts the hd digits (packed u16 LDS atomics); one
+//       scan gives every (wave, digit) its offset
+//   A1  each wave walks its slice in order, 64 containers at a time; a container's place
+//       among equal digits in the 64 is a match mask of ballots, so X[p] = index in
+//       stable hd order with no barrier inside the pass
+//   B   every hd bucket (~630 containers in config 4) is sorted by ld by one wave, stable
+//       the same way, and written straight to its final positions; the bucket's window of
+//       each output array is a few KB, so its scattered dword stores merge in L2
+// A scenario without such digits takes the generic fallback (ss_generic) in the same workgroup.
+// Round 3 ranked against the whole batch's values instead: two streaming passes over every
+// container (k_value_bitmap, k_digits: 0.85 ms per 4096-scenario step) before the sort.
+// LDS: max(X u16[C], the rank tables' 96 KB) + ld u8[C] + [16][256] u16 + tables -> C <= ~50.3k.
 constexpr uint32_t SS_DIG = 256;     // digits per dimension (dense ranks)
 constexpr uint32_t SS_WAVES = 16;
 constexpr uint32_t SS_CHUNKS = 50;   // 64-container chunks per wave slice: C <= 16 x 50 x 64 = 51,200
+constexpr uint32_t SS_LB = 25;       // chunks whose loads are in flight together (R, A0)
 constexpr uint32_t SS_REG = 16;      // B: buckets of up to 64 x SS_REG containers are reordered in registers
 constexpr size_t SS_LDS_CAP = 160 * 1024;
-constexpr uint32_t DG_TABLE_WORDS = 4096;  // k_digits stages rank tables of at most this many words in LDS
+constexpr uint32_t SR_W = RANK_WORDS;                  // bitmap words per dimension (values < 2^18)
+constexpr size_t SR_BYTES = (size_t)SR_W * (4 + 2) * 2;  // bitmaps u32 + prefix counts u16, both dimensions
 
 __host__ __device__ static inline size_t ss_align16(size_t b) { return (b + 15) & ~(size_t)15; }
-// X, LD, WH [16][256] u16, HS/HB u32 [256], MV u32 [256], MB/CB u8 [256], NEXT
-static inline size_t ss_lds_bytes(uint32_t C) {
-    return ss_align16((size_t)C * 2) + ss_align16(C) + SS_WAVES * SS_DIG * 2 + 2 * SS_DIG * 4 + SS_DIG * 4 +
-           2 * SS_DIG + 16;
+__host__ __device__ static inline size_t ss_xr_bytes(uint32_t C) {
+    return ss_align16((size_t)C * 2 > SR_BYTES ? (size_t)C * 2 : SR_BYTES);
 }
-
-// u16 digit pair per container: hd | ld << 8 (dense ranks, ascending = descending demand)
-// The distinct counts, bounds and eligibility are device values (cnt, k_rank_tables /
-// k_thresholds): a batch the digits cannot express (cnt[CN_ELIG] = 0) leaves at once and
-// k_scen_sort takes its generic fallback.
-__global__ __launch_bounds__(256) void k_digits(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
-                                                size_t n, const uint32_t *__restrict__ cnt,
-                                                const uint32_t *__restrict__ bmc, const uint32_t *__restrict__ prc,
-                                                const uint32_t *__restrict__ bmm, const uint32_t *__restrict__ prm,
-                                                uint16_t *__restrict__ dig) {
-    extern __shared__ uint32_t dgt[];  // [wc] bm, [wc] pre (cpu), [wm] bm, [wm] pre (mem) when they fit
-    if (!cnt[CN_ELIG]) return;
-    const uint32_t dc = cnt[CN_DC], dm = cnt[CN_DM];
-    const uint32_t wc = (cnt[CN_MAXC] >> 5) + 1u, wm = (cnt[CN_MAXM] >> 5) + 1u;
-    const bool lds = wc + wm <= DG_TABLE_WORDS;
-    if (lds) {
-        for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) { dgt[i] = bmc[i]; dgt[wc + i] = prc[i]; }
-        for (uint32_t i = threadIdx.x; i < wm; i += blockDim.x) { dgt[2 * wc + i] = bmm[i]; dgt[2 * wc + wm + i] = prm[i]; }
-        __syncthreads();
-    }
-    const uint32_t *tbc = lds ? dgt : bmc, *tpc = lds ? dgt + wc : prc;
-    const uint32_t *tbm = lds ? dgt + 2 * wc : bmm, *tpm = lds ? dgt + 2 * wc + wm : prm;
-    auto digit = [&](uint32_t c, uint32_t m) -> uint32_t {
-        const uint32_t rc = tpc[c >> 5] + (uint32_t)__popc(tbc[c >> 5] & ((1u << (c & 31)) - 1u));
-        const uint32_t rm = tpm[m >> 5] + (uint32_t)__popc(tbm[m >> 5] & ((1u << (m & 31)) - 1u));
-        return (dc - 1u - rc) | ((dm - 1u - rm) << 8);
-    };
-    const size_t stride = (size_t)gridDim.x * blockDim.x, t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t head = 0;
-    if (((reinterpret_cast<uintptr_t>(cpu) | reinterpret_cast<uintptr_t>(mem)) & 15u) == 0 &&
-        (reinterpret_cast<uintptr_t>(dig) & 7u) == 0) {
-        const uint4 *c4 = reinterpret_cast<const uint4 *>(cpu), *m4 = reinterpret_cast<const uint4 *>(mem);
-        uint2 *d4 = reinterpret_cast<uint2 *>(dig);
-        for (size_t i = t; i < n / 4; i += stride) {
-            const uint4 c = c4[i], m = m4[i];
-            uint2 o;
-            o.x = digit(c.x, m.x) | (digit(c.y, m.y) << 16);
-            o.y = digit(c.z, m.z) | (digit(c.w, m.w) << 16);
-            d4[i] = o;
-        }
-        head = n / 4 * 4;
-    }
-    for (size_t i = head + t; i < n; i += stride) dig[i] = (uint16_t)digit(cpu[i], mem[i]);
+// XR (X / rank tables), LD, WH [16][256] u16, HS/HB u32 [256], MV/CV u32 [256], MB/CB u8 [256], NEXT [4]
+static inline size_t ss_lds_bytes(uint32_t C) {
+    return ss_xr_bytes(C) + ss_align16(C) + SS_WAVES * SS_DIG * 2 + 2 * SS_DIG * 4 + 2 * SS_DIG * 4 + 2 * SS_DIG + 16;
 }
 
 struct ScenSortArgs {
     uint32_t C, kpack;
-    const uint32_t *cnt;                     // distinct counts, bounds, eligibility (device, CN_*)
-    const uint16_t *dig;                     // [S][C] k_digits
-    const uint32_t *cval, *mval;             // ascending distinct values
-    const uint32_t *cpu, *mem;               // [S][C] the raw demands (the generic fallback)
+    const uint32_t *cpu, *mem;               // [S][C] the demands
     uint32_t *order, *s_cpu, *s_mem, *s_idx; // [S][C] FFD order, sorted cpu / mem / position word
     const uint32_t *T;                       // [2 FP_BUCKETS] bucket thresholds (cpu, then mem; device)
 };
@@ -439,96 +384,186 @@ __device__ void ss_generic(const ScenSortArgs &a, uint16_t *X, uint16_t *WH, uin
 
 #ifdef FP_PIPE_STATS
 // diagnostics build: k_scen_sort phase cycles summed over workgroups (fp_debug_sort_stats):
-// [0] A0 [1] offsets [2] A1 [3] B (until the last wave) [4] B busy summed over waves [5] workgroups
-// [6] largest bucket [7] whole kernel
+// [0] R (ranks) [1] A0 + offsets [2] A1 [3] B (until the last wave) [4] B busy summed over waves
+// [5] workgroups [6] largest bucket [7] whole kernel
 __device__ unsigned long long g_sort_stats[8];
 #define SS_CLK() __builtin_amdgcn_s_memtime()
 #else
 #define SS_CLK() 0ull
 #endif
 
+// exclusive block scan of one u32 per thread (1024 threads); `part` holds 16 entries
+__device__ __forceinline__ uint32_t ss_block_excl(uint32_t v, uint32_t *part, uint32_t lane, uint32_t w,
+                                                  uint32_t &total) {
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        inc += lane >= (uint32_t)o ? y : 0u;
+    }
+    if (lane == 63) part[w] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+#pragma unroll
+    for (uint32_t ww = 0; ww < SS_WAVES; ++ww) {
+        const uint32_t x = part[ww];
+        before += ww < w ? x : 0u;
+        total += x;
+    }
+    return before + inc - v;
+}
+
 __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char ssm[];
-    const uint32_t C = a.C, dc = a.cnt[CN_DC], dm = a.cnt[CN_DM];
+    const uint32_t C = a.C;
     uint16_t *X = reinterpret_cast<uint16_t *>(ssm);
-    uint8_t *LD = ssm + ss_align16((size_t)C * 2);
+    uint8_t *LD = ssm + ss_xr_bytes(C);
     uint16_t *WH = reinterpret_cast<uint16_t *>(LD + ss_align16(C));     // [wave][digit]
     uint32_t *HS = reinterpret_cast<uint32_t *>(WH + SS_WAVES * SS_DIG);  // bucket starts
     uint32_t *HB = HS + SS_DIG;                                          // bucket ends
     uint32_t *MV = HB + SS_DIG;                                          // mem value per ld
-    uint8_t *MB = reinterpret_cast<uint8_t *>(MV + SS_DIG);              // mem bucket per ld
+    uint32_t *CV = MV + SS_DIG;                                          // cpu value per hd
+    uint8_t *MB = reinterpret_cast<uint8_t *>(CV + SS_DIG);              // mem bucket per ld
     uint8_t *CB = MB + SS_DIG;                                           // cpu bucket per hd
-    uint32_t *NEXT = reinterpret_cast<uint32_t *>(CB + SS_DIG);
+    uint32_t *NEXT = reinterpret_cast<uint32_t *>(CB + SS_DIG);          // [0] next bucket [1] a value >= 2^18
+    // R's tables live where X will be (X is first written in A1)
+    uint32_t *BMC = reinterpret_cast<uint32_t *>(ssm), *BMM = BMC + SR_W;
+    uint16_t *PRC = reinterpret_cast<uint16_t *>(BMM + SR_W), *PRM = PRC + SR_W;
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
     const size_t cb = (size_t)blockIdx.x * C;
-    const uint16_t *dig = a.dig + cb;
-    // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
-    const uint32_t hbits = dc > 1 ? 32u - (uint32_t)__builtin_clz(dc - 1u) : 0u;
-    const uint32_t lbits = dm > 1 ? 32u - (uint32_t)__builtin_clz(dm - 1u) : 0u;
-    if (!a.cnt[CN_ELIG]) {  // no dense ranks for this batch (device flag, k_thresholds)
-        ss_generic(a, X, WH, HS, HB, cb, C);
-        return;
-    }
-
-    for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
-    if (t < SS_DIG) {
-        const uint32_t mv = t < dm ? a.mval[dm - 1u - t] : 0u;
-        MV[t] = mv;
-        MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, mv) : 0;
-        CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, a.cval[dc - 1u - t]) : 0;
-    }
-    if (t == 0) NEXT[0] = 0u;
+    const uint32_t *cpu = a.cpu + cb, *mem = a.mem + cb;
     const unsigned long long ck0 = SS_CLK();
-    __syncthreads();
 
-    // A0: per-wave hd counts over the wave's slice [s0, s1), ld into LDS
-    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
-    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
-    uint16_t *myrow = WH + w * SS_DIG;
-    // the wave's whole slice (<= SS_CHUNKS x 64 digit pairs) is loaded at once and kept in
-    // registers for A1: one round trip instead of one per 8 chunks (round 3), and no second read
-    uint32_t dv[SS_CHUNKS];
+    // ---- R: the scenario's distinct values and dense ranks ----
+    for (uint32_t i = t; i < 2 * SR_W; i += blockDim.x) BMC[i] = 0u;
+    for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
+    if (t < 4) NEXT[t] = 0u;
+    __syncthreads();
+    {
+        bool big = false;
+        for (uint32_t k0 = 0; k0 < SS_CHUNKS; k0 += SS_LB) {  // coalesced, SS_LB x 2 loads in flight
+            uint32_t cv[SS_LB], mv[SS_LB];
 #pragma unroll
-    for (uint32_t k = 0; k < SS_CHUNKS; ++k) {
-        const uint32_t p = s0 + 64 * k + lane;
-        dv[k] = p < s1 ? (uint32_t)__builtin_nontemporal_load(&dig[p]) : 0u;
+            for (uint32_t k = 0; k < SS_LB; ++k) {
+                const uint32_t i = t + blockDim.x * (k0 + k);
+                cv[k] = i < C ? __builtin_nontemporal_load(&cpu[i]) : 0u;
+                mv[k] = i < C ? __builtin_nontemporal_load(&mem[i]) : 0u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < SS_LB; ++k) {
+                if (t + blockDim.x * (k0 + k) < C) {
+                    const uint32_t c = cv[k], m = mv[k];
+                    if ((c | m) >= RANK_MAX_VALUE) {
+                        big = true;
+                    } else {  // test before set: most bits are already there
+                        const uint32_t bc = 1u << (c & 31), bm = 1u << (m & 31);
+                        if (!(BMC[c >> 5] & bc)) atomicOr(&BMC[c >> 5], bc);
+                        if (!(BMM[m >> 5] & bm)) atomicOr(&BMM[m >> 5], bm);
+                    }
+                }
+            }
+        }
+        if (__ballot(big) && lane == 0) atomicOr(&NEXT[1], 1u);
     }
+    __syncthreads();
+    // prefix popcounts: thread t owns words [8t, 8t + 8) of both bitmaps (SR_W = 8 x 1024)
+    static_assert(SR_W == 8 * 1024, "rank words per thread");
+    uint32_t bw[8], bx[8], sc = 0, sm = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < SS_CHUNKS; ++k) {
-        const uint32_t p = s0 + 64 * k + lane;
-        if (p < s1) {
-            LD[p] = (uint8_t)(dv[k] >> 8);
-            ss_inc16(myrow, dv[k] & 0xFFu);
+    for (uint32_t j = 0; j < 8; ++j) {
+        bw[j] = BMC[8 * t + j];
+        bx[j] = BMM[8 * t + j];
+        sc += (uint32_t)__popc(bw[j]);
+        sm += (uint32_t)__popc(bx[j]);
+    }
+    uint32_t dc = 0, dm = 0;
+    uint32_t pc = ss_block_excl(sc, HS, lane, w, dc);
+    __syncthreads();  // HS reused by the second scan
+    uint32_t pm = ss_block_excl(sm, HB, lane, w, dm);
+    const bool elig = NEXT[1] == 0u && dc >= 1u && dm >= 1u && dc <= SS_DIG && dm <= SS_DIG;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        PRC[8 * t + j] = (uint16_t)pc;
+        PRM[8 * t + j] = (uint16_t)pm;
+        if (elig) {  // the value of every rank, flipped to digit order (<= 256 bits in all)
+            for (uint32_t x = bw[j]; x; x &= x - 1) CV[dc - 1u - pc++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
+            for (uint32_t x = bx[j]; x; x &= x - 1) MV[dm - 1u - pm++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
+        } else {
+            pc += (uint32_t)__popc(bw[j]);
+            pm += (uint32_t)__popc(bx[j]);
         }
     }
     __syncthreads();
+    if (!elig) {  // more than 256 distinct values in a dimension, or a value >= 2^18 (uniform)
+        ss_generic(a, X, WH, HS, HB, cb, C);
+        return;
+    }
+    if (t < SS_DIG) {
+        MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, MV[t]) : 0;
+        CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, CV[t]) : 0;
+    }
     const unsigned long long ck1 = SS_CLK();
+    // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
+    const uint32_t hbits = dc > 1 ? 32u - (uint32_t)__builtin_clz(dc - 1u) : 0u;
+    const uint32_t lbits = dm > 1 ? 32u - (uint32_t)__builtin_clz(dm - 1u) : 0u;
+
+    // ---- A0: the wave's slice [s0, s1) ranked into digit pairs (kept in registers, two per
+    // dword), ld into LDS, per-wave hd counts ----
+    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
+    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
+    uint16_t *myrow = WH + w * SS_DIG;
+    uint32_t dvp[SS_CHUNKS / 2];
+#pragma unroll
+    for (uint32_t k = 0; k < SS_CHUNKS / 2; ++k) dvp[k] = 0u;
+#pragma unroll
+    for (uint32_t k0 = 0; k0 < SS_CHUNKS; k0 += SS_LB) {
+        uint32_t cv[SS_LB], mv[SS_LB];
+#pragma unroll
+        for (uint32_t k = 0; k < SS_LB; ++k) {
+            const uint32_t p = s0 + 64 * (k0 + k) + lane;
+            cv[k] = p < s1 ? __builtin_nontemporal_load(&cpu[p]) : 0u;
+            mv[k] = p < s1 ? __builtin_nontemporal_load(&mem[p]) : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SS_LB; ++k) {
+            const uint32_t p = s0 + 64 * (k0 + k) + lane;
+            if (p < s1) {
+                const uint32_t c = cv[k], m = mv[k];
+                const uint32_t rc = PRC[c >> 5] + (uint32_t)__popc(BMC[c >> 5] & ((1u << (c & 31)) - 1u));
+                const uint32_t rm = PRM[m >> 5] + (uint32_t)__popc(BMM[m >> 5] & ((1u << (m & 31)) - 1u));
+                const uint32_t hd = dc - 1u - rc, ld = dm - 1u - rm;
+                LD[p] = (uint8_t)ld;
+                ss_inc16(myrow, hd);
+                dvp[(k0 + k) >> 1] |= hd << (16u * ((k0 + k) & 1u));
+            }
+        }
+    }
+    __syncthreads();
     ss_offsets(WH, HS, HB, t, lane, w);
     const unsigned long long ck2 = SS_CLK();
 
-    // A1: stable scatter by hd, each wave over its own slice (digits from A0's registers)
-    {
+    // ---- A1: stable scatter by hd, each wave over its own slice (digits from A0's registers) ----
 #pragma unroll
-        for (uint32_t k = 0; k < SS_CHUNKS; ++k) {
-            const uint32_t p0 = s0 + 64 * k;
-            if (p0 >= s1) break;  // wave-uniform
-            const uint32_t p = p0 + lane;
-            const bool valid = p < s1;
-            const uint32_t d = dv[k] & 0xFFu;
-            const uint64_t m = ss_match(d, valid, hbits);
-            const uint32_t off = myrow[d];
-            if (valid) {
-                if ((m & lt) == 0) myrow[d] = (uint16_t)(off + __popcll(m));
-                X[off + (uint32_t)__popcll(m & lt)] = (uint16_t)p;
-            }
+    for (uint32_t k = 0; k < SS_CHUNKS; ++k) {
+        const uint32_t p0 = s0 + 64 * k;
+        if (p0 >= s1) break;  // wave-uniform
+        const uint32_t p = p0 + lane;
+        const bool valid = p < s1;
+        const uint32_t d = (dvp[k >> 1] >> (16u * (k & 1u))) & 0xFFFFu;
+        const uint64_t m = ss_match(d, valid, hbits);
+        const uint32_t off = myrow[d];
+        if (valid) {
+            if ((m & lt) == 0) myrow[d] = (uint16_t)(off + __popcll(m));
+            X[off + (uint32_t)__popcll(m & lt)] = (uint16_t)p;
         }
     }
     __syncthreads();
     const unsigned long long ck3 = SS_CLK();
     uint32_t big = 0;
 
-    // B: each hd bucket sorted by ld by one wave and written out
+    // ---- B: each hd bucket sorted by ld by one wave and written out ----
     while (true) {
         uint32_t d = 0;
         if (lane == 0) d = atomicAdd(NEXT, 1u);
@@ -541,7 +576,7 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
         // fences keep those accesses in order (s_waitcnt lgkmcnt(0), no compiler reordering)
         reinterpret_cast<ss_u64a *>(myrow)[lane] = 0ull;  // 4 digits per lane
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        const uint32_t cv = a.cval[dc - 1u - d];
+        const uint32_t cv = CV[d];
         const uint32_t kbc = a.kpack ? (uint32_t)CB[d] << 21 : 0u;
         if (hi - lo <= 64 * SS_REG) {
             // the bucket in registers: count, scan, reorder X[lo, hi) in place, then write the
@@ -636,12 +671,12 @@ __device__ void value_thresholds(const uint32_t *v, uint32_t d, uint32_t *T) {
 }
 
 // The pipeline's bucket thresholds, thr[0, K) cpu and [K, 2K) mem (thread 0: cpu, 1: mem): spread
-// over the batch's distinct values when it has dense ranks -- every bucket then spans about D / 31
+// over the sample's distinct values when they are below 2^18 -- every bucket then spans about D / 31
 // distinct values (config 4: 79 cpu and 256 mem values -> 2.5 and 8 per bucket; geometric steps
 // spanned 9 and 43 at the top of the range, where most demands lie, and loose buckets cost exact
-// checks that miss) -- else geometric from the smallest positive to the largest demand.  Also the
-// LDS sort's eligibility: dense ranks with at most 256 values per dimension.  Any ascending choice
-// with T[0] = 0 is exact: the thresholds only decide how tight the candidate masks are.
+// checks that miss) -- else geometric from the smallest positive to the largest demand.  Any
+// ascending choice with T[0] = 0 is exact: the thresholds only decide how tight the candidate masks
+// are, so a sample of the batch sets them.
 __global__ void k_thresholds(uint32_t *__restrict__ cnt, const uint32_t *__restrict__ cval,
                              const uint32_t *__restrict__ mval, uint32_t *__restrict__ thr) {
     const uint32_t d = threadIdx.x;
@@ -655,8 +690,6 @@ __global__ void k_thresholds(uint32_t *__restrict__ cnt, const uint32_t *__restr
         fp_thresholds(lo == 0xFFFFFFFFu ? 1u : lo, hi, T);
     }
     for (int k = 0; k < FP_BUCKETS; ++k) thr[d * FP_BUCKETS + k] = T[k];
-    if (d == 0)
-        cnt[CN_ELIG] = ranks && cnt[CN_DC] >= 1 && cnt[CN_DM] >= 1 && cnt[CN_DC] <= SS_DIG && cnt[CN_DM] <= SS_DIG;
 }
 
 }  // namespace
@@ -681,6 +714,9 @@ static inline unsigned grid_for(size_t n, unsigned block) {
 
 // Workspace bytes fp_dev_place_batch takes for S scenarios of C containers x N nodes
 // (sort_tmp: the sorts' scratch share of it).
+// scenarios whose values set the bucket thresholds (k_value_bitmap's sample)
+constexpr uint32_t THR_SAMPLE = 8;
+
 static int place_ws_need(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, size_t *need, size_t *sort_tmp_out) {
     hipStream_t st = c->stream;
     const size_t SC = (size_t)S * C;
@@ -754,18 +790,21 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !rbm || !rpre || !rval || !rcnt || !thr)
         return FP_ENOMEM;
 
-    // ---- 1-2: values, dense ranks, bounds, thresholds, LDS-sort eligibility (device) ----
+    // ---- 1-2: the bucket thresholds (device), from the distinct values and bounds of a sample:
+    // the first THR_SAMPLE scenarios (any ascending thresholds with T[0] = 0 are exact; they only
+    // set how tight the pipeline's candidate masks are) ----
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_SORT, &ev);
     FP_HIP(hipMemsetAsync(rbm, 0, 2 * RANK_WORDS * 4, st));
     FP_HIP(hipMemsetAsync(rcnt, 0, CN_WORDS * 4, st));
     FP_HIP(hipMemsetAsync(rcnt + CN_MINC, 0xFF, 8, st));  // the minima start at 0xFFFFFFFF
     {
-        unsigned gb = grid_for((SC + 3) / 4, 256);
+        const size_t n = (size_t)(S < THR_SAMPLE ? S : THR_SAMPLE) * C;
+        unsigned gb = grid_for((n + 3) / 4, 256);
         if (gb > 1024) gb = 1024;  // each block merges its bitmaps once
         FP_HIP(hipFuncSetAttribute((const void *)k_value_bitmap, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(2 * RANK_WORDS * 4)));
-        k_value_bitmap<<<gb, 256, 2 * RANK_WORDS * 4, st>>>(b->cpu_m, b->mem_mib, SC, rbm, rbm + RANK_WORDS, rcnt);
+        k_value_bitmap<<<gb, 256, 2 * RANK_WORDS * 4, st>>>(b->cpu_m, b->mem_mib, n, rbm, rbm + RANK_WORDS, rcnt);
         FP_HIP(hipGetLastError());
         k_rank_tables<<<2, 1024, 0, st>>>(rbm, rbm + RANK_WORDS, RANK_WORDS, RANK_WORDS, rpre, rpre + RANK_WORDS, rval,
                                           rval + RANK_MAX_VALUE, rcnt);
@@ -773,23 +812,12 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         k_thresholds<<<1, 64, 0, st>>>(rcnt, rval, rval + RANK_MAX_VALUE, thr);
         FP_HIP(hipGetLastError());
     }
-    // ---- 3a: per-scenario LDS sort (scenarios of at most ~50k containers; host-known).  A batch
+    // ---- 3a: per-scenario LDS sort (scenarios of at most ~50k containers; host-known).  A scenario
     // without dense ranks of <= 256 values per dimension takes k_scen_sort's generic fallback,
-    // chosen on the device.  FP_OPT_SCEN_SORT = 0 keeps the radix path. ----
+    // chosen in its workgroup.  FP_OPT_SCEN_SORT = 0 keeps the radix path. ----
     if (ss_lds_bytes(C) <= SS_LDS_CAP && C <= SS_WAVES * SS_CHUNKS * 64 && fp_opt(c, FP_OPT_SCEN_SORT, 1) != 0) {
-        uint16_t *dig = (uint16_t *)keys_in;  // SC x u16 digit pairs (keys_in holds SC x 8 B)
-        {
-            const size_t tl = (size_t)DG_TABLE_WORDS * 8;  // rank tables staged when they fit (device choice)
-            FP_HIP(hipFuncSetAttribute((const void *)k_digits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
-            k_digits<<<grid_for((SC + 3) / 4, 256) < 4096 ? grid_for((SC + 3) / 4, 256) : 4096, 256, tl, st>>>(
-                b->cpu_m, b->mem_mib, SC, rcnt, rbm, rpre, rbm + RANK_WORDS, rpre + RANK_WORDS, dig);
-            FP_HIP(hipGetLastError());
-        }
         ScenSortArgs sa;
         sa.C = C; sa.kpack = fp_pipe_kpack(c, C);
-        sa.cnt = rcnt;
-        sa.dig = dig;
-        sa.cval = rval; sa.mval = rval + RANK_MAX_VALUE;
         sa.cpu = b->cpu_m; sa.mem = b->mem_mib;
         fp_pipe_soa soa;
         if (int rs = fp_pipe_soa_take(c, SC, &soa)) return rs;
@@ -808,8 +836,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     // range on the host (FP_OPT_SEGSORT no longer changes anything: several scenarios are always
     // sorted as segments, one scenario device-wide) ----
     const uint64_t full = 0xFFFFFFFFull;
-    k_make_keys<uint64_t><<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, 64, 32, full, full, nullptr,
-                                                             nullptr, nullptr, nullptr, keys_in, vals_in);
+    k_make_keys<<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, keys_in, vals_in);
     FP_HIP(hipGetLastError());
     if (S == 1) {
         FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in, vals_out, SC, 0, 64, st));

@@ -43,7 +43,7 @@ def main():
     wg = max(buf[5], 1)
     us = lambda x: x / wg / ghz.value / 1e3  # noqa: E731  per workgroup (scenario), microseconds
     print(f"S={S} C={C} N={N} clock {ghz.value:.3f} GHz, sort path avg {sort_ms / max(n, 1):.3f} ms, workgroups {buf[5]}")
-    print(f"per scenario us: A0 {us(buf[0]):.2f}  offsets {us(buf[1]):.2f}  A1 {us(buf[2]):.2f}  "
+    print(f"per scenario us: R {us(buf[0]):.2f}  A0+offsets {us(buf[1]):.2f}  A1 {us(buf[2]):.2f}  "
           f"B {us(buf[3]):.2f} (busy per wave {us(buf[4]) / 16:.2f})  total {us(buf[7]):.2f}  largest bucket {buf[6]}")
     print(f"resident: 256 CUs x 1 workgroup -> {S / 256:.0f} rounds x {us(buf[7]):.1f} us = "
           f"{S / 256 * us(buf[7]) / 1e3:.3f} ms")
