@@ -457,9 +457,9 @@ def test_config4_bench_size_batch(planner, O):
 @pytest.mark.parametrize("case", ["all_equal", "cpu_const", "mem_const", "rank_limit", "past_rank_limit",
                                   "dense_wide", "zero_mix"])
 def test_ffd_sort_key_compression(case, planner, O):
-    """The FFD order uses dense value ranks as key fields when both maxima are below
-    2^18 (fp_place.hip k_value_bitmap/k_rank_tables) and the raw values otherwise;
-    either way the order, and so the plan, must be the oracle's."""
+    """The LDS sort ranks a scenario's values into digits when it has at most 256 distinct
+    values per dimension, all below 2^18 (fp_place.hip k_scen_sort), and sorts the raw values
+    otherwise (its generic fallback); either way the order, and so the plan, must be the oracle's."""
     rng = np.random.default_rng(hash(case) & 0xFFFF)
     C, N = 3000, 400
     lim = 1 << 18
@@ -695,8 +695,8 @@ def test_levelize_deep_chain_three_sort_passes(planner, O):
 
 @pytest.mark.parametrize("S,C,dv", [(3, 50_000, 300), (2, 20_000, 257), (4, 8_000, 256)])
 def test_scen_sort_generic_fallback(S, C, dv, planner, O):
-    """Scenarios that fit the per-scenario LDS sort but whose batch has more than 256 distinct cpu
-    values (dv > 256) take k_scen_sort's generic LSD fallback, chosen on the device (no read-back);
+    """Scenarios that fit the per-scenario LDS sort but have more than 256 distinct cpu values
+    (dv > 256) take k_scen_sort's generic LSD fallback, chosen in the workgroup (no read-back);
     dv = 256 stays on the digit path.  Plans, reasons and costs must be the oracle's either way."""
     rng = np.random.default_rng(C + dv)
     N = 2_000
@@ -719,3 +719,36 @@ def test_scen_sort_generic_fallback(S, C, dv, planner, O):
         assert int(cost[s]) == O.cost(ea, N, 7 + s)
         for i in (0, 1, 3):
             assert np.array_equal(after[i][s * N:(s + 1) * N], eafter[i])
+
+
+def test_scen_sort_mixed_eligibility(planner, O):
+    """Each workgroup of the LDS sort ranks its own scenario: in one batch, scenarios with dense
+    digits (<= 256 values per dimension), with too many distinct values, with a value >= 2^18 and
+    with a single value take the digit sort or the generic fallback side by side."""
+    rng = np.random.default_rng(23)
+    S, C, N = 8, 6000, 700
+    conts, nodes = [], []
+    for s in range(S):
+        c, n = O.gen_scenario(SEED + 77, s, C, N, 7)
+        c = [np.array(a, np.uint32) for a in c]
+        kind = s % 4
+        if kind == 0:    # dense digits
+            c[0] = rng.choice(np.arange(50, 5000, 25), C).astype(np.uint32)
+            c[1] = rng.choice(np.arange(64, 64 * 200, 64), C).astype(np.uint32)
+        elif kind == 1:  # too many distinct mem values
+            c[1] = rng.integers(1, 100_000, C).astype(np.uint32)
+        elif kind == 2:  # one demand past the rank tables
+            c[0][rng.integers(0, C)] = (1 << 18) + 5
+        else:            # one value per dimension
+            c[0][:] = 300; c[1][:] = 4096
+        conts.append(c)
+        nodes.append(n)
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    assign, reason, cost, after = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
+                                                      [cat(nodes, i) for i in range(5)], scen_base=40)
+    for s in range(S):
+        ea, er, eafter, _ = O.place(conts[s], nodes[s])
+        assert np.array_equal(assign[s * C:(s + 1) * C], ea), s
+        assert np.array_equal(reason[s * C:(s + 1) * C], er), s
+        assert int(cost[s]) == O.cost(ea, N, 40 + s)
+        assert np.array_equal(after[0][s * N:(s + 1) * N], eafter[0])
