@@ -48,10 +48,18 @@ def test_levelize_golden(golden, planner):
         assert ncyc == sum(1 for x in case["level"] if x == NONE)
 
 
-@pytest.mark.parametrize("params", [(20, 30, 6, 50, 3), (0, 0, 4, 100, 5), (200, 3, 2, 300, 0), (1, 1, 0, 0, 0)])
-def test_levelize_random_dags(params, planner, O):
+@pytest.mark.parametrize("small", [1, 0])
+@pytest.mark.parametrize("params", [(20, 30, 6, 50, 3), (0, 0, 4, 100, 5), (200, 3, 2, 300, 0), (1, 1, 0, 0, 0),
+                                    (4, 50, 3, 100, 4)])
+def test_levelize_random_dags(params, small, planner, O):
+    """Generated DAGs, through the one-launch small-graph levelizer (<= 512 vertices) and with it
+    off (FP_OPT_LEVEL_SMALL = 0: the asynchronous path)."""
     rp, col, hd = O.gen_dag(SEED + sum(params), *params)
-    level, order, ncyc = planner.levelize(rp, col, hd)
+    planner.set_option("level_small", small)
+    try:
+        level, order, ncyc = planner.levelize(rp, col, hd)
+    finally:
+        planner.set_option("level_small")
     el, eo, en = O.levelize(rp, col, hd)
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
@@ -200,6 +208,25 @@ def test_levelize_config5_full_size(tree, planner, O):
     el, eo, en = O.levelize(rp, col, hd)
     assert ncyc == en == 999
     assert np.array_equal(level, el) and np.array_equal(order, eo)
+
+
+@pytest.mark.parametrize("V", [511, 512, 513])
+def test_levelize_small_graph_limits(V, planner, O):
+    """Around the small-graph limit (512 vertices, fp_order.hip k_lvl_small): a chain as deep as
+    the graph (levels up to V with has_deps), fan-out side edges, a 3-cycle with a tail behind it,
+    duplicate edges and a self loop."""
+    rng = np.random.default_rng(V)
+    edges = [(v, v + 1) for v in range(V - 8)]
+    edges += [(int(a), int(b)) for a, b in zip(rng.integers(0, V - 8, 300), rng.integers(0, V - 8, 300)) if a < b]
+    edges += [(V - 6, V - 5), (V - 5, V - 4), (V - 4, V - 6), (V - 4, V - 3), (V - 2, V - 2), (0, 3), (0, 3)]
+    rp, col = _csr(V, edges)
+    hd = np.zeros(V, np.uint8)
+    hd[np.unique(col)] = 1
+    hd[0] = 1
+    level, order, ncyc = planner.levelize(rp, col, hd)
+    el, eo, en = O.levelize(rp, col, hd)
+    assert en == 5  # the 3-cycle, its tail, the self loop
+    assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
 def test_levelize_rejects_corrupt_csr(planner):
