@@ -249,7 +249,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
-                                           uint32_t &nhit, uint32_t sys) {
+                                           uint32_t &nhit, uint32_t sys, unsigned long long (&gst)[4]) {
     constexpr uint32_t pf_max = G <= SYS_MAX_G ? PF_MAX_NARROW : PF_MAX_WIDE;
     (
         [&] {
@@ -278,6 +278,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
             }
             if (q) {
                 uint64_t touched = 0;
+                const unsigned long long gc0 = STAT_CLK();
                 // long queues (a filling group): the systolic loop, else the serial one
                 // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
                 if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
@@ -286,6 +287,8 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                 else
                     fpp_group_x<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                        req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
+                const unsigned long long gc1 = STAT_CLK();
+                if (STAT_ON) { gst[0] += gc1 - gc0; gst[2] += 1; gst[3] += (uint32_t)__builtin_popcountll(touched); }
                 if (touched) {
                     const bool me = (touched >> lane) & 1ull;
                     if (gs < 32) used |= me ? (1u << gs) : 0u;
@@ -307,6 +310,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                       ~clr);
                     }
                 }
+                if (STAT_ON) gst[1] += STAT_CLK() - gc1;
             }
         }(),
         ...);
@@ -465,7 +469,8 @@ k_ffd_pipe(const PipeArgs a) {
     uint32_t opend = 0;
     uint32_t n_used = 0, n_rej = 0;
     uint32_t st_spin_in = 0, st_spin_out = 0, st_visits = 0, st_checks = 0, st_hits = 0, st_batches = 0;
-    unsigned long long ck_in = 0, ck_pre = 0, ck_cand = 0, ck_fwd = 0, ck_wait = 0;
+    unsigned long long ck_in = 0, ck_pre = 0, ck_cand = 0, ck_fwd = 0, ck_wait = 0, ck_gx = 0, ck_gu = 0;
+    uint32_t st_queues = 0, st_touched = 0;
     const unsigned long long ck_t0 = STAT_CLK();
     unsigned long long ck_a, ck_b;
 #ifdef FP_PIPE_STATS
@@ -647,12 +652,16 @@ k_ffd_pipe(const PipeArgs a) {
             // exact: a stale mask is a superset): config 3 (1 x 1M x 100k) ran 127 -> 104 ms
             // without the update, while config 4's 20-group stages need it (57 vs 66 ms)
             uint32_t nchk = 0, nhit = 0;
+            unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
             if (todo)
                 fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
-                                       __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys);
-            if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
+                                       __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
+            if (STAT_ON) {
+                st_checks += nchk; st_hits += nhit;
+                ck_gx += gst[0]; ck_gu += gst[1]; st_queues += (uint32_t)gst[2]; st_touched += (uint32_t)gst[3];
+            }
         }
         if (zs_g < G) {
             // all-zero containers change no record: each takes the first schedulable node
@@ -724,6 +733,7 @@ k_ffd_pipe(const PipeArgs a) {
                 ofill = 0;
                 opend = 0;
             }
+            ck_b = STAT_CLK(); ck_fwd += ck_b - ck_a; ck_a = ck_b;
             continue;
         }
         if (!has_out) {
@@ -829,8 +839,11 @@ k_ffd_pipe(const PipeArgs a) {
         STAT_ADD(st_slot, 3, st_batches); STAT_ADD(st_slot, 4, st_spin_in); STAT_ADD(st_slot, 5, st_spin_out);
         STAT_ADD(st_slot, 8, ck_in); STAT_ADD(st_slot, 9, ck_pre); STAT_ADD(st_slot, 10, ck_cand); STAT_ADD(st_slot, 11, ck_fwd);
         STAT_ADD(st_slot, 12, ck_wait); STAT_ADD(st_slot, 13, STAT_CLK() - ck_t0);
+        STAT_ADD(st_slot, 6, ck_gx); STAT_ADD(st_slot, 7, ck_gu); STAT_ADD(st_slot, 14, st_queues);
+        STAT_ADD(st_slot, 15, st_touched);
     }
-    (void)ck_t0; (void)ck_in; (void)ck_pre; (void)ck_cand; (void)ck_fwd; (void)ck_wait;
+    (void)ck_t0; (void)ck_in; (void)ck_pre; (void)ck_cand; (void)ck_fwd; (void)ck_wait; (void)ck_gx; (void)ck_gu;
+    (void)st_queues; (void)st_touched;
     (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
     // write the tile's node state back (registers -> HBM)
 #pragma unroll

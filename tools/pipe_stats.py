@@ -57,8 +57,8 @@ def main():
             continue
         f = lambda x: x / S / 1e6  # noqa: E731
         print(f"{w:5d} {f(v[8]):18.2f} {f(v[9]):8.2f} {f(v[10]):10.2f} {f(v[11]):5.2f} {f(v[12]):9.2f} {f(v[13]):6.2f}"
-              f"   | {v[10]/max(v[1],1):8.0f}   phaseA {f(v[6]):6.2f} phaseB {f(v[7]):6.2f} clean {v[14]/S:7.0f}"
-              f" dirty_cache {v[15]/S:7.0f}")
+              f"   | {v[10]/max(v[1],1):8.0f}   in cand_loop: checks {f(v[6]):6.2f} mask upkeep {f(v[7]):6.2f}"
+              f"  queues/scen {v[14]/S:7.0f} touched/scen {v[15]/S:7.0f}")
 
 
 
