@@ -333,7 +333,14 @@ constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
 // ms, r03af), req / conf of link input loaded after the prescan (15.45 vs 15.08 ms, r03ac).
 template <uint32_t G, uint32_t BLK>
 __global__ __launch_bounds__(BLK, BLK == 64 ? (G == 12 ? WIDE12_WAVES : WIDE_WAVES) : 1) void
-k_ffd_pipe(const PipeArgs a) {
+k_ffd_pipe(const PipeArgs a_arg) {
+    // the arguments are read through the kernarg segment (memory), not promoted to SGPRs for the
+    // whole kernel: held in SGPRs they spilled into VGPR lanes (781 v_readlane vs 296)
+#if defined(__HIP_DEVICE_COMPILE__)
+    const PipeArgs &a = *(const PipeArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    const PipeArgs &a = a_arg;  // the host pass only type-checks the body
+#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = a.W, R = a.R, B = a.B;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

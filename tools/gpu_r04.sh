@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU session steps (run on the box via gpurun from the repo root):
-#   tools/gpu_r04.sh <tag> <step>...   steps: ubench | tests:<pytest -k expr> | alltests | sweep:<opt>:<values>:<loads> | sortstats | bench
+#   tools/gpu_r04.sh <tag> <step>...   steps: ubench | tests:<pytest -k expr> | alltests | sweep:<opt>:<values>:<loads> | sortstats | pipestats | bench
 set -o pipefail
 root=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$root" || exit 1
@@ -23,6 +23,10 @@ for step in "$@"; do
       timeout -k 10 400 python -u tools/sys_sweep.py --opt "$opt" --values "$vals" --loads "$loads" --reps 3 \
         > gpurun_out/${tag}_sweep_${opt}.jsonl 2>&1 || { echo "sweep failed"; tail -20 gpurun_out/${tag}_sweep_${opt}.jsonl; exit 1; }
       cut -c1-200 gpurun_out/${tag}_sweep_${opt}.jsonl ;;
+    pipestats)
+      FLEETPLACE_LIB=$PWD/fleetflow_amd/libfleetplace_stats.so timeout -k 10 200 python -u tools/pipe_stats.py 4096 \
+        > gpurun_out/${tag}_pipestats_c4.txt 2>&1 || { echo "pipestats failed"; tail -20 gpurun_out/${tag}_pipestats_c4.txt; exit 1; }
+      cat gpurun_out/${tag}_pipestats_c4.txt ;;
     sortstats)
       timeout -k 10 300 python -u tools/sort_stats.py > gpurun_out/${tag}_sortstats.txt 2>&1 \
         || { echo "sortstats failed"; tail -20 gpurun_out/${tag}_sortstats.txt; exit 1; }
