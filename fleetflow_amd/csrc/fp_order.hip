@@ -349,7 +349,11 @@ __global__ void k_tree_jump(const uint64_t *__restrict__ lin, uint64_t *__restri
         }
         lout[u] = x;
     }
-    if (__ballot(open) && (threadIdx.x & 63) == 0) atomicOr(&flags[k], 1u);
+    // one atomic per block at most, and none once the flag is up: a per-wave atomic on this one
+    // word serialised ~15k times per round (74 us a round for config 5)
+    if (__syncthreads_or(open) && threadIdx.x == 0 && !__hip_atomic_load(&flags[k], __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT))
+        atomicOr(&flags[k], 1u);
 }
 
 // final levels of the source-rooted vertices, and the largest of them (ctl maxlvl)
@@ -369,8 +373,18 @@ __global__ void k_tree_levels(const uint64_t *lk0, const uint64_t *lk1, const ui
             level[u] = lvl;
         }
     }
+    // block maximum, then one atomic per block that raises the global one (a per-wave atomicMax
+    // on this single word serialised: 181 us for config 5)
     for (int o = 32; o > 0; o >>= 1) lvl = max(lvl, (uint32_t)__shfl_xor((int)lvl, o));
-    if ((threadIdx.x & 63) == 0 && lvl) atomicMax(&ctl[26 * kCtlStride], lvl);
+    __shared__ uint32_t wmax[4];
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = lvl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = 0;
+        for (uint32_t i = 0; i < (blockDim.x + 63) / 64; ++i) m = max(m, wmax[i]);
+        if (m > __hip_atomic_load(&ctl[26 * kCtlStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(&ctl[26 * kCtlStride], m);
+    }
 }
 
 // Every edge from a source-rooted parent into a join is relaxed on the join's packed state word of

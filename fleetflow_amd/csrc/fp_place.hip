@@ -85,23 +85,36 @@ __global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict
         head = n4 * 4;
     }
     for (size_t i = head + t; i < n; i += stride) add(cpu[i], mem[i]);
-    if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(&cnt[CN_OVER], 1u);
+    // block reductions, then at most one atomic per block and word, and none that would change
+    // nothing: per-wave atomics on these few words serialise at the memory side
+    const bool anybig = __syncthreads_or(big);
     for (int o = 32; o > 0; o >>= 1) {
         bxc = max(bxc, (uint32_t)__shfl_xor((int)bxc, o));
         bxm = max(bxm, (uint32_t)__shfl_xor((int)bxm, o));
         bnc = min(bnc, (uint32_t)__shfl_xor((int)bnc, o));
         bnm = min(bnm, (uint32_t)__shfl_xor((int)bnm, o));
     }
+    __shared__ uint32_t wb[4][4];  // [wave][max c, max m, min c, min m], 256 threads
     if ((threadIdx.x & 63) == 0) {
-        atomicMax(&cnt[CN_MAXC], bxc);
-        atomicMax(&cnt[CN_MAXM], bxm);
-        atomicMin(&cnt[CN_MINC], bnc);
-        atomicMin(&cnt[CN_MINM], bnm);
+        wb[threadIdx.x >> 6][0] = bxc; wb[threadIdx.x >> 6][1] = bxm;
+        wb[threadIdx.x >> 6][2] = bnc; wb[threadIdx.x >> 6][3] = bnm;
     }
     __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < 4; ++w) {
+            bxc = max(bxc, wb[w][0]); bxm = max(bxm, wb[w][1]);
+            bnc = min(bnc, wb[w][2]); bnm = min(bnm, wb[w][3]);
+        }
+        auto ld = [](uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        if (anybig && !ld(&cnt[CN_OVER])) atomicOr(&cnt[CN_OVER], 1u);
+        if (bxc > ld(&cnt[CN_MAXC])) atomicMax(&cnt[CN_MAXC], bxc);
+        if (bxm > ld(&cnt[CN_MAXM])) atomicMax(&cnt[CN_MAXM], bxm);
+        if (bnc < ld(&cnt[CN_MINC])) atomicMin(&cnt[CN_MINC], bnc);
+        if (bnm < ld(&cnt[CN_MINM])) atomicMin(&cnt[CN_MINM], bnm);
+    }
     for (uint32_t i = threadIdx.x; i < RANK_WORDS; i += blockDim.x) {
-        if (lc[i]) atomicOr(&gbc[i], lc[i]);
-        if (lm[i]) atomicOr(&gbm[i], lm[i]);
+        if (lc[i] & ~gbc[i]) atomicOr(&gbc[i], lc[i]);
+        if (lm[i] & ~gbm[i]) atomicOr(&gbm[i], lm[i]);
     }
 }
 
