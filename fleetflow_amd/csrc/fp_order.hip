@@ -259,7 +259,7 @@ __global__ void k_edge_hop(uint32_t E, const uint4 *__restrict__ rec, const uint
 __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
                                  const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t *__restrict__ level,
                                  uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
-                                 bool pk, bool push_src, const uint32_t *__restrict__ bad) {
+                                 bool pk, const uint32_t *__restrict__ bad) {
     if (*bad) return;
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = v < V;
@@ -272,7 +272,7 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
         state[v] = ((uint64_t)l0 << 32) | indeg[v];
         level[v] = src && deg == 0 ? l0 : FP_NONE;
     }
-    const bool push = push_src && src && deg != 0;  // else k_tree_relax expands the sources' trees
+    const bool push = src && deg != 0;
     const uint64_t m = __ballot(push);
     if (!m) return;
     const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(m);
@@ -283,166 +283,6 @@ __global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t 
     if (push)
         Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
             ((uint64_t)(pk ? l0 << 8 : l0) << 32) | v;
-}
-
-// ---- in-tree pre-pass (pointer jumping) ---------------------------------------------------
-// A vertex with exactly one parent has level(parent) + 1, so following the only-parent edges up
-// from v reaches the root of v's in-tree, r(v) (a vertex with no parent or several), at distance
-// d(v), and level(v) = level(r(v)) + d(v).  Wyllie's pointer jumping finds (r, d) for every vertex
-// in ceil(log2 depth) synchronous rounds.  Trees rooted at a SOURCE then have final levels at once
-// (level(r) = has_deps(r); k_tree_levels), and every edge from them into a join (a vertex with
-// several parents) is relaxed by one edge-parallel pass (k_tree_relax) -- config 5's 500-deep
-// chains cost 9 rounds instead of 500 dependent hops in k_lvl_async.  The async kernel then starts
-// from the joins that pass made ready and walks only the trees rooted at joins; it never meets a
-// source-rooted vertex (such a vertex's only in-edge comes from its source-rooted parent).
-// Link word per vertex: low 32 bits = r, high = d | flags.  The rounds ping-pong between two
-// buffers with plain loads (round k reads buffer k & 1): in place, with agent-scope atomic loads and
-// stores, a round ran 182 us for config 5 against ~10 for a plain streaming pass.  A vertex on (or
-// below) a cycle of only-parent edges never reaches a root: its distance doubles every round, and
-// at >= V it is marked LK_CYC (never final, as Kahn leaves it).
-constexpr uint32_t LK_TERM = 1u << 31, LK_SRC = 1u << 30, LK_CYC = 1u << 29, LK_DIST = LK_CYC - 1u;
-constexpr uint32_t kTreeRounds = 32;  // flag words (rounds <= bits(V) + 1 <= 31)
-
-// roots (in-degree != 1) link to themselves, terminal; an only-parent child links to its parent
-// at distance 1 (exactly one edge names it, so exactly one store); esrc[e] = the edge's parent
-__global__ void k_tree_init(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t V,
-                            const uint32_t *__restrict__ indeg, uint64_t *__restrict__ link,
-                            uint32_t *__restrict__ esrc, const uint32_t *__restrict__ bad) {
-    if (*bad) return;
-    const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= V) return;
-    const uint32_t du = indeg[u];
-    if (du != 1u) link[u] = ((uint64_t)(LK_TERM | (du == 0u ? LK_SRC : 0u)) << 32) | u;
-    const uint32_t e1 = row_ptr[u + 1];
-    for (uint32_t e = row_ptr[u]; e < e1; ++e) {
-        const uint32_t w = col[e];
-        esrc[e] = (uint32_t)u;
-        if (indeg[w] == 1u) link[w] = (1ull << 32) | u;
-    }
-}
-
-// first round whose output left no vertex open: its output buffer holds the final links
-__device__ __forceinline__ const uint64_t *tree_final(const uint64_t *const *lk, const uint32_t *flags,
-                                                      uint32_t rounds) {
-    uint32_t k = 0;
-    while (k + 1 < rounds && flags[k]) ++k;
-    return lk[(k + 1) & 1u];
-}
-
-// one jumping round: (r, d) <- (r(r), d + d(r)), from buffer k & 1 into the other; round k > 0 runs
-// only if round k - 1 left a vertex open (flags[k - 1]), so the host enqueues every round V could
-// need and reads nothing back
-__global__ void k_tree_jump(const uint64_t *__restrict__ lin, uint64_t *__restrict__ lout, uint32_t V, uint32_t k,
-                            uint32_t *__restrict__ flags, const uint32_t *__restrict__ bad) {
-    if (*bad || (k && !flags[k - 1])) return;
-    const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool open = false;
-    if (u < V) {
-        uint64_t x = lin[u];
-        if (!((x >> 32) & LK_TERM)) {
-            const uint64_t y = lin[(uint32_t)x];
-            const uint32_t hy = (uint32_t)(y >> 32);
-            const uint32_t d = ((uint32_t)(x >> 32) & LK_DIST) + (hy & LK_DIST);
-            if ((hy & LK_CYC) || d >= V) x = (uint64_t)(LK_TERM | LK_CYC) << 32;
-            else x = ((uint64_t)((hy & (LK_TERM | LK_SRC)) | d) << 32) | (uint32_t)y;
-            open = !((x >> 32) & LK_TERM);
-        }
-        lout[u] = x;
-    }
-    // one atomic per block at most, and none once the flag is up: a per-wave atomic on this one
-    // word serialised ~15k times per round (74 us a round for config 5)
-    if (__syncthreads_or(open) && threadIdx.x == 0 && !__hip_atomic_load(&flags[k], __ATOMIC_RELAXED,
-                                                                        __HIP_MEMORY_SCOPE_AGENT))
-        atomicOr(&flags[k], 1u);
-}
-
-// final levels of the source-rooted vertices, and the largest of them (ctl maxlvl)
-__global__ void k_tree_levels(const uint64_t *lk0, const uint64_t *lk1, const uint32_t *__restrict__ flags,
-                              uint32_t rounds, const uint8_t *__restrict__ hd, uint32_t V, uint32_t *__restrict__ level,
-                              uint32_t *__restrict__ ctl, const uint32_t *__restrict__ bad) {
-    if (*bad) return;
-    const uint64_t *const lkb[2] = {lk0, lk1};
-    const uint64_t *link = tree_final(lkb, flags, rounds);
-    const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t lvl = 0;
-    if (u < V) {
-        const uint64_t x = link[u];
-        const uint32_t hx = (uint32_t)(x >> 32);
-        if ((hx & (LK_SRC | LK_CYC)) == LK_SRC) {
-            lvl = (hd[(uint32_t)x] ? 1u : 0u) + (hx & LK_DIST);
-            level[u] = lvl;
-        }
-    }
-    // block maximum, then one atomic per block that raises the global one (a per-wave atomicMax
-    // on this single word serialised: 181 us for config 5)
-    for (int o = 32; o > 0; o >>= 1) lvl = max(lvl, (uint32_t)__shfl_xor((int)lvl, o));
-    __shared__ uint32_t wmax[4];
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = lvl;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t m = 0;
-        for (uint32_t i = 0; i < (blockDim.x + 63) / 64; ++i) m = max(m, wmax[i]);
-        if (m > __hip_atomic_load(&ctl[26 * kCtlStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            atomicMax(&ctl[26 * kCtlStride], m);
-    }
-}
-
-// Every edge from a source-rooted parent into a join is relaxed on the join's packed state word of
-// k_lvl_async (level max, parents - 1), one edge per thread; a join whose last parent this was goes
-// to the queues.  A join may also finish inside k_lvl_async: each edge is relaxed exactly once, here
-// or there.  The CAS guesses the join's initial word (has_deps, in-degree): the first parent to
-// arrive needs one round trip.
-__global__ void k_tree_relax(const uint32_t *__restrict__ col, const uint32_t *__restrict__ esrc, uint32_t E,
-                             const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg, const uint64_t *lk0,
-                             const uint64_t *lk1, const uint32_t *__restrict__ flags, uint32_t rounds, uint32_t V,
-                             uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
-                             bool pk, const uint32_t *__restrict__ bad) {
-    if (*bad) return;
-    const uint64_t *const lkb[2] = {lk0, lk1};
-    const uint64_t *link = tree_final(lkb, flags, rounds);
-    const uint32_t lane = threadIdx.x & 63;
-    for (size_t e0 = (size_t)blockIdx.x * blockDim.x; e0 < E; e0 += (size_t)gridDim.x * blockDim.x) {
-        const size_t e = e0 + threadIdx.x;
-        bool rdy = false;
-        uint32_t w = 0, wl = 0;
-        if (e < E) {
-            w = col[e];
-            const uint32_t dw = indeg[w];
-            if (dw != 1u) {
-                const uint64_t x = link[esrc[e]];
-                const uint32_t hx = (uint32_t)(x >> 32);
-                if ((hx & (LK_SRC | LK_CYC)) == LK_SRC) {
-                    const uint32_t lvl = (hd[(uint32_t)x] ? 1u : 0u) + (hx & LK_DIST);
-                    uint64_t exp = ((uint64_t)(hd[w] ? 1u : 0u) << 32) | dw, cur = 0;
-                    while (true) {
-                        const uint32_t nl = max((uint32_t)(exp >> 32), lvl + 1u);
-                        const uint64_t nv = ((uint64_t)nl << 32) | (uint32_t)((uint32_t)exp - 1u);
-                        uint64_t obs = exp;
-                        if (__hip_atomic_compare_exchange_strong(&state[w], &obs, nv, __ATOMIC_RELAXED,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                            cur = nv;
-                            break;
-                        }
-                        exp = obs;
-                    }
-                    rdy = (uint32_t)cur == 0u;
-                    wl = (uint32_t)(cur >> 32);
-                }
-            }
-        }
-        const uint64_t m = __ballot(rdy);
-        if (m) {
-            const uint32_t sh = (uint32_t)((e0 >> 6) % kShards);
-            const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&ctl[(kShards + sh) * kCtlStride], (uint32_t)__popcll(m));
-            base = __shfl(base, (int)leader);
-            if (rdy)
-                __hip_atomic_store(&Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))],
-                                   ((uint64_t)(pk ? wl << 8 : wl) << 32) | w, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
@@ -1113,11 +953,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
     }
-    // FP_OPT_TREE_JUMP (on by default): the in-tree pre-pass before k_lvl_async
-    const bool tree = !level_sync && E && fp_opt(c, FP_OPT_TREE_JUMP, 1) != 0;
-    const size_t async_ws = level_sync ? 0
-                                       : (size_t)V * 8 * (1 + kShards) + (size_t)E * 16 * kHops + kCtlWords * 4 +
-                                             (tree ? (size_t)V * 16 + (size_t)E * 4 + kTreeRounds * 4 + 768 : 0);
+    const size_t async_ws = level_sync ? 0 : (size_t)V * 8 * (1 + kShards) + (size_t)E * 16 * kHops + kCtlWords * 4;
     const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 : 0;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + async_ws + cs_ws + 23 * 256);
     if (rc) return rc;
@@ -1158,37 +994,14 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
         uint4 *erec = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
         uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16 * (kHops - 1)) : nullptr;
-        uint64_t *const link[2] = {tree ? (uint64_t *)fp_ws_take(c, (size_t)V * 8) : nullptr,
-                                   tree ? (uint64_t *)fp_ws_take(c, (size_t)V * 8) : nullptr};
-        uint32_t *esrc = tree ? (uint32_t *)fp_ws_take(c, (size_t)E * 4) : nullptr;
-        uint32_t *tflags = tree ? (uint32_t *)fp_ws_take(c, kTreeRounds * 4) : nullptr;
-        if (!state || !Q || !actl || (E && (!erec || !erec2)) || (tree && (!link[0] || !link[1] || !esrc || !tflags)))
-            return FP_ENOMEM;
+        if (!state || !Q || !actl || (E && (!erec || !erec2))) return FP_ENOMEM;
         FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
         FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
         // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
         const bool pk = V < (1u << 24);
         k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl,
-                                                             pk, !tree, bad);
+                                                             pk, bad);
         FP_HIP(hipGetLastError());
-        if (tree) {
-            FP_HIP(hipMemsetAsync(tflags, 0, kTreeRounds * 4, st));
-            k_tree_init<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, g->col, V, indeg, link[0], esrc, bad);
-            FP_HIP(hipGetLastError());
-            // every open distance doubles per round: after bits(V) + 1 rounds it is >= V
-            const uint32_t rounds = fp_bitwidth((uint64_t)V) + 1u;
-            for (uint32_t k = 0; k < rounds; ++k) {
-                k_tree_jump<<<blocks_for(V, 256), 256, 0, st>>>(link[k & 1], link[(k + 1) & 1], V, k, tflags, bad);
-                FP_HIP(hipGetLastError());
-            }
-            k_tree_levels<<<blocks_for(V, 256), 256, 0, st>>>(link[0], link[1], tflags, rounds, g->has_deps, V, level,
-                                                              actl, bad);
-            FP_HIP(hipGetLastError());
-            const unsigned eg = blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192;
-            k_tree_relax<<<eg, 256, 0, st>>>(g->col, esrc, E, g->has_deps, indeg, link[0], link[1], tflags, rounds, V,
-                                             state, Q, actl, pk, bad);
-            FP_HIP(hipGetLastError());
-        }
         if (E) {
             const unsigned eg = blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192;
             k_edge_rec<<<eg, 256, 0, st>>>(g->row_ptr, g->col, E, V, indeg, erec, bad);

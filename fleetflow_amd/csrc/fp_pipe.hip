@@ -1085,9 +1085,8 @@ __global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restr
 // through LDS in chunks of PL_CHUNK and picks its positions' values out of the chunk that holds
 // them (level the same way first, for the CYCLE bits).  k_gather_payload's two random 4-B reads
 // per container ran at the L2 request rate (2.2 ms for 4096 x 50k).  C <= PL_MAX_C.
-constexpr uint32_t PL_THREADS = 1024, PL_H = 50, PL_MAX_C = PL_THREADS * PL_H;
+constexpr uint32_t PL_THREADS = 1024, PL_H = 25, PL_MAX_C = PL_THREADS * PL_H * 2;
 constexpr uint32_t PL_CHUNK = 18 * 1024;  // (req, conf) pairs: 144 KB of LDS
-constexpr uint32_t PL_PER = PL_CHUNK / PL_THREADS;  // chunk entries per thread
 __global__ __launch_bounds__(1024) void k_payload_lds(uint32_t C, const uint32_t *__restrict__ order,
                                                       const uint32_t *__restrict__ req,
                                                       const uint32_t *__restrict__ conf,
@@ -1101,75 +1100,55 @@ __global__ __launch_bounds__(1024) void k_payload_lds(uint32_t C, const uint32_t
     const size_t cb = (size_t)blockIdx.x * C;
     const uint32_t sm0 = summ ? summ[(size_t)blockIdx.x * 4] : 0xFFFFFFFFu;
     const uint32_t sm1 = summ ? summ[(size_t)blockIdx.x * 4 + 1] : 0u;
-    {
-        const uint32_t pbase = t;
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t pbase = h * PL_THREADS * PL_H + t;
+        if (h * PL_THREADS * PL_H >= C) break;  // uniform: every thread meets the same barriers
         uint32_t o[PL_H];
 #pragma unroll
         for (uint32_t j = 0; j < PL_H; ++j) {
             const uint32_t p = pbase + PL_THREADS * j;
             o[j] = p < C ? __builtin_nontemporal_load(&order[cb + p]) : 0xFFFFFFFFu;
         }
-        uint64_t cy = 0;
+        uint32_t vr[PL_H], vf[PL_H];
+        uint32_t cy = 0;
         if (level) {
             for (uint32_t a0 = 0; a0 < C; a0 += 2 * PL_CHUNK) {
                 const uint32_t n = C - a0 < 2 * PL_CHUNK ? C - a0 : 2 * PL_CHUNK;
                 __syncthreads();
-                {  // every load of the chunk in flight at once (one round trip per chunk)
-                    uint32_t x[2 * PL_PER];
-#pragma unroll
-                    for (uint32_t k = 0; k < 2 * PL_PER; ++k) {
-                        const uint32_t i = t + k * PL_THREADS;
-                        x[k] = i < n ? __builtin_nontemporal_load(&level[cb + a0 + i]) : 0u;
-                    }
-#pragma unroll
-                    for (uint32_t k = 0; k < 2 * PL_PER; ++k)
-                        if (t + k * PL_THREADS < n) pl_lds[t + k * PL_THREADS] = x[k];
-                }
+#pragma unroll 4
+                for (uint32_t i = t; i < n; i += PL_THREADS) pl_lds[i] = __builtin_nontemporal_load(&level[cb + a0 + i]);
                 __syncthreads();
 #pragma unroll
                 for (uint32_t j = 0; j < PL_H; ++j) {
                     const uint32_t d = o[j] - a0;
-                    if (d < n) cy |= (uint64_t)(pl_lds[d] == FP_NONE) << j;
+                    if (d < n) cy |= (uint32_t)(pl_lds[d] == FP_NONE) << j;
                 }
             }
         }
         for (uint32_t a0 = 0; a0 < C; a0 += PL_CHUNK) {
             const uint32_t n = C - a0 < PL_CHUNK ? C - a0 : PL_CHUNK;
             __syncthreads();
-            {  // every load of the chunk in flight at once: the workgroup is alone on its CU, so
-               // the chunk's round trips, not bandwidth, set the time (4 in flight: 1.16 ms per
-               // 4096-scenario step)
-                uint32_t x[PL_PER], y[PL_PER];
-#pragma unroll
-                for (uint32_t k = 0; k < PL_PER; ++k) {
-                    const uint32_t i = t + k * PL_THREADS;
-                    x[k] = i < n ? __builtin_nontemporal_load(&req[cb + a0 + i]) : 0u;
-                    y[k] = i < n ? __builtin_nontemporal_load(&conf[cb + a0 + i]) : 0u;
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < PL_PER; ++k)
-                    if (t + k * PL_THREADS < n) pl_lds2[t + k * PL_THREADS] = make_uint2(x[k], y[k]);
-            }
+#pragma unroll 4
+            for (uint32_t i = t; i < n; i += PL_THREADS)
+                pl_lds2[i] = make_uint2(__builtin_nontemporal_load(&req[cb + a0 + i]), __builtin_nontemporal_load(&conf[cb + a0 + i]));
             __syncthreads();
-            // each position's pair lies in exactly one chunk: written as soon as it is found (no
-            // per-position registers held across the chunks).  `pt` is opaque per chunk so that
-            // the 50 output addresses are not hoisted out of the chunk loop (300 VGPRs: spills)
-            uint32_t pt = pbase;
-            asm volatile("" : "+v"(pt));
 #pragma unroll
             for (uint32_t j = 0; j < PL_H; ++j) {
                 const uint32_t d = o[j] - a0;
-                if (d < n) {
-                    const uint2 v = pl_lds2[d];
-                    const size_t p = cb + pt + PL_THREADS * j;
-                    uint32_t r = v.x;
-                    const bool c = (cy >> j) & 1u, x = ((r & ~sm0) | (v.y & sm1)) != 0u;
-                    if (c) r = FP_REASON_CYCLE;
-                    else if (summ && x) r = FP_REASON_NOFIT;
-                    __builtin_nontemporal_store(r, &s_req[p]);
-                    __builtin_nontemporal_store(v.y, &s_conf[p]);
-                    if (c || (summ && x)) s_idx[p] |= CYC;
-                }
+                if (d < n) { const uint2 x = pl_lds2[d]; vr[j] = x.x; vf[j] = x.y; }
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < PL_H; ++j) {
+            const uint32_t p = pbase + PL_THREADS * j;
+            if (p < C) {
+                uint32_t r = vr[j];
+                const bool c = (cy >> j) & 1u, x = ((r & ~sm0) | (vf[j] & sm1)) != 0u;
+                if (c) r = FP_REASON_CYCLE;
+                else if (summ && x) r = FP_REASON_NOFIT;
+                __builtin_nontemporal_store(r, &s_req[cb + p]);
+                __builtin_nontemporal_store(vf[j], &s_conf[cb + p]);
+                if (c || (summ && x)) s_idx[cb + p] |= CYC;
             }
         }
     }
@@ -1198,7 +1177,7 @@ __global__ __launch_bounds__(1024) void k_unsort(uint32_t C, uint32_t H, uint32_
     const uint32_t s = blockIdx.x / H, h = blockIdx.x % H;
     const uint32_t lo = h * span, hi = min(C, lo + span);
     const size_t cb = (size_t)s * C;
-    constexpr uint32_t U = 25;  // loads in flight per thread (a 50k scenario: two round trips)
+    constexpr uint32_t U = 8;  // loads in flight per thread
     for (uint32_t p0 = threadIdx.x; p0 < C; p0 += blockDim.x * U) {
         uint32_t j[U], av[U];
         uint8_t rv[U];

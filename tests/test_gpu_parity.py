@@ -74,9 +74,8 @@ def _csr(V, edges):
     return rp, col
 
 
-@pytest.mark.parametrize("tree", [1, 0])
 @pytest.mark.parametrize("shape", ["star", "dup_and_self", "long_chain_fanout", "wide_hubs"])
-def test_levelize_async_shapes(shape, tree, planner, O):
+def test_levelize_async_shapes(shape, planner, O):
     """Shapes aimed at the asynchronous levelizer's paths: wave-cooperative expansion
     (a vertex with thousands of dependents), duplicate edges and self loops (CAS
     retries, CYCLE), chain continuation with fan-out side edges, many hubs."""
@@ -101,22 +100,16 @@ def test_levelize_async_shapes(shape, tree, planner, O):
     hd = np.zeros(V, np.uint8)
     hd[np.unique(col)] = 1
     hd[rng.integers(0, V, V // 10)] = 1  # deps outside the target set
-    planner.set_option("tree_jump", tree)
-    try:
-        level, order, ncyc = planner.levelize(rp, col, hd)
-    finally:
-        planner.set_option("tree_jump")
+    level, order, ncyc = planner.levelize(rp, col, hd)
     el, eo, en = O.levelize(rp, col, hd)
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
-@pytest.mark.parametrize("tree", [1, 0])
 @pytest.mark.parametrize("shape", ["ring_with_tails", "join_then_chain", "random_forest", "cycle_fed_tree"])
-def test_levelize_tree_shapes(shape, tree, planner, O):
-    """The in-tree pre-pass (fp_order.hip k_tree_*): rings of only-parent edges with chains
-    hanging off them (never final: LK_CYC), a deep chain below a join (walked by k_lvl_async,
-    not pre-resolved), a 200k-vertex random forest (every vertex source-rooted, depth ~ hundreds),
-    and a tree fed by a cycle member; pre-pass on and off give the oracle's levels and order."""
+def test_levelize_only_parent_shapes(shape, planner, O):
+    """Only-parent structures for k_lvl_async's chain hops: rings of only-parent edges with chains
+    hanging off them (never final), a deep chain below a join, a 200k-vertex random forest, and a
+    tree fed by a cycle member."""
     rng = np.random.default_rng(11)
     if shape == "ring_with_tails":
         V = 20_000
@@ -142,11 +135,7 @@ def test_levelize_tree_shapes(shape, tree, planner, O):
     hd = np.zeros(V, np.uint8)
     hd[np.unique(col)] = 1
     hd[rng.integers(0, V, V // 7)] = 1
-    planner.set_option("tree_jump", tree)
-    try:
-        level, order, ncyc = planner.levelize(rp, col, hd)
-    finally:
-        planner.set_option("tree_jump")
+    level, order, ncyc = planner.levelize(rp, col, hd)
     el, eo, en = O.levelize(rp, col, hd)
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
@@ -196,15 +185,10 @@ def test_levelize_async_unpacked_entries(planner, O):
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
-@pytest.mark.parametrize("tree", [1, 0])
-def test_levelize_config5_full_size(tree, planner, O):
+def test_levelize_config5_full_size(planner, O):
     """BASELINE config 5: 1M vertices (1000 chains x 500 + 50 layers x 10k), 333 3-cycles."""
     rp, col, hd = O.gen_dag(SEED + 5, 1000, 500, 50, 10_000, 333)
-    planner.set_option("tree_jump", tree)
-    try:
-        level, order, ncyc = planner.levelize(rp, col, hd)
-    finally:
-        planner.set_option("tree_jump")
+    level, order, ncyc = planner.levelize(rp, col, hd)
     el, eo, en = O.levelize(rp, col, hd)
     assert ncyc == en == 999
     assert np.array_equal(level, el) and np.array_equal(order, eo)
