@@ -195,7 +195,10 @@ constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B l
 constexpr uint64_t kQEmpty = ~0ull;
 constexpr uint32_t kCoopEdges = 16;       // edges left at which the wave expands a vertex together
 constexpr uint32_t kLaneEdges = 1;        // edges a lane relaxes per round
-constexpr uint32_t kHops = 4;             // levels a lane may jump per round along only-parent first edges
+#ifndef FP_LVL_HOPS
+#define FP_LVL_HOPS 4
+#endif
+constexpr uint32_t kHops = FP_LVL_HOPS;    // levels a lane may jump per round along only-parent first edges
 constexpr uint32_t kPush = kLaneEdges + kHops;  // queue entries a lane may push per round
 // ctl layout (u32 index): head[s] = s*32, tail[s] = (8+s)*32, done[s] = (16+s)*32,
 // fin = 24*32, abort = 25*32, maxlvl = 26*32
