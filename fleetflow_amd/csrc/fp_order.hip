@@ -195,10 +195,9 @@ constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B l
 constexpr uint64_t kQEmpty = ~0ull;
 constexpr uint32_t kCoopEdges = 16;       // edges left at which the wave expands a vertex together
 constexpr uint32_t kLaneEdges = 1;        // edges a lane relaxes per round
-#ifndef FP_LVL_HOPS
-#define FP_LVL_HOPS 4
-#endif
-constexpr uint32_t kHops = FP_LVL_HOPS;    // levels a lane may jump per round along only-parent first edges
+// levels a lane may jump per round along only-parent first edges: 4 (config 5 0.84 ms; 6 hops 0.86, 8 hops
+// 0.92 -- more records to build and load per round, profiles/r04m_lvl_hops_ab.txt)
+constexpr uint32_t kHops = 4;
 constexpr uint32_t kPush = kLaneEdges + kHops;  // queue entries a lane may push per round
 // ctl layout (u32 index): head[s] = s*32, tail[s] = (8+s)*32, done[s] = (16+s)*32,
 // fin = 24*32, abort = 25*32, maxlvl = 26*32

@@ -42,6 +42,14 @@ __device__ unsigned long long g_pipe_stats[16 * 16];
 #define STAT_ADD(w, i, v) atomicAdd(&g_pipe_stats[(w) * 16 + (i)], (unsigned long long)(v))
 #define STAT_CLK() __builtin_amdgcn_s_memtime()
 #define STAT_ON 1
+// per group-queue timers ([6] check loop, [7] mask upkeep cycles): two more s_memtime per queue,
+// which doubles config 3's diagnostics time, so only with FP_PIPE_STATS_FINE
+// (tools/build_variant.sh _statsfine -DFP_PIPE_STATS -DFP_PIPE_STATS_FINE)
+#ifdef FP_PIPE_STATS_FINE
+#define STAT_GCLK() __builtin_amdgcn_s_memtime()
+#else
+#define STAT_GCLK() 0ull
+#endif
 // per-batch timeline of scenario 0: [stage][batch] = (t_in_ready, t_prescan, t_cand, t_out_done)
 constexpr int TL_B = 2048;
 __device__ unsigned long long g_pipe_tl[16 * TL_B * 8];
@@ -53,6 +61,7 @@ __device__ unsigned long long g_stage_span[SPAN_MAX * 8];
 #else
 #define STAT_ADD(w, i, v) ((void)0)
 #define STAT_CLK() 0ull
+#define STAT_GCLK() 0ull
 #define STAT_ON 0
 #endif
 
@@ -278,7 +287,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
             }
             if (q) {
                 uint64_t touched = 0;
-                const unsigned long long gc0 = STAT_CLK();
+                const unsigned long long gc0 = STAT_GCLK();
                 // long queues (a filling group): the systolic loop, else the serial one
                 // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
                 if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
@@ -287,7 +296,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                 else
                     fpp_group_x<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                        req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
-                const unsigned long long gc1 = STAT_CLK();
+                const unsigned long long gc1 = STAT_GCLK();
                 if (STAT_ON) { gst[0] += gc1 - gc0; gst[2] += 1; gst[3] += (uint32_t)__builtin_popcountll(touched); }
                 if (touched) {
                     const bool me = (touched >> lane) & 1ull;
@@ -310,7 +319,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                       ~clr);
                     }
                 }
-                if (STAT_ON) gst[1] += STAT_CLK() - gc1;
+                if (STAT_ON) gst[1] += STAT_GCLK() - gc1;
             }
         }(),
         ...);
