@@ -1,7 +1,11 @@
 #!/bin/bash
 # One GPU session: error-path tests (isolated, short limit), the -m gpu suite, the bench
 # (config 4 at 4096 + config 3 leg + CPU baseline), then the rocprofv3 passes.
-# Usage: tools/gpu_round.sh <tag> [steps...]   steps: errors tests bench scale prof (default: errors tests bench prof)
+# Usage: tools/gpu_round.sh <tag> [steps...]
+#   steps: errors tests bench scale prof kt lvl sortstats pipestats model (default: errors tests bench prof)
+#   kt = config-4 kernel trace (tools/ktrace.sh), lvl = config-5 levelizer timing + kernel stats
+#   (tools/gpu_lvl.sh), sortstats / pipestats / model = diagnostics-build runs (k_scen_sort phases,
+#   per-stage pipeline counters at 4096 scenarios, the latency model of tools/pipe_model.py)
 set -o pipefail
 tag=${1:?tag}; shift
 steps=${*:-errors tests bench prof}
@@ -30,9 +34,20 @@ for s in $steps; do
       done ;;
     prof)
       timeout -k 10 1000 bash tools/profile.sh $tag || { echo "profile failed"; exit 1; } ;;
-    stats)
-      timeout -k 10 300 python -u tools/pipe_stats.py 512 > ${log}_pipe_stats.txt 2>&1 || { echo "stats failed"; tail ${log}_pipe_stats.txt; exit 1; }
-      cat ${log}_pipe_stats.txt ;;
+    kt)
+      tools/ktrace.sh $tag > ${log}_kt.txt 2>&1 || { echo "kt failed"; tail -20 ${log}_kt.txt; exit 1; }
+      cat ${log}_kt.txt ;;
+    lvl)
+      tools/gpu_lvl.sh $tag || { echo "lvl failed"; exit 1; } ;;
+    sortstats)
+      timeout -k 10 300 python -u tools/sort_stats.py > ${log}_sortstats.txt 2>&1 || { echo "sortstats failed"; tail ${log}_sortstats.txt; exit 1; }
+      cat ${log}_sortstats.txt ;;
+    pipestats|stats)
+      timeout -k 10 300 python -u tools/pipe_stats.py 4096 > ${log}_pipestats.txt 2>&1 || { echo "pipestats failed"; tail ${log}_pipestats.txt; exit 1; }
+      cat ${log}_pipestats.txt ;;
+    model)
+      timeout -k 10 400 python -u tools/pipe_model.py ${log}_pipe_model.json > ${log}_pipe_model.log 2>&1 || { echo "model failed"; tail ${log}_pipe_model.log; exit 1; } ;;
+    *) echo "unknown step $s"; exit 2 ;;
   esac
 done
 echo "gpu_round $tag done: $steps"
