@@ -345,7 +345,9 @@ __global__ __launch_bounds__(BLK, BLK == 64 ? (G == 12 ? WIDE12_WAVES : WIDE_WAV
 k_ffd_pipe(const PipeArgs a_arg) {
     // the arguments are read through the kernarg segment (memory), not promoted to SGPRs for the
     // whole kernel: held in SGPRs they spilled into VGPR lanes (781 v_readlane vs 296)
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(FP_AB_NARROW_BYVAL)
+    const PipeArgs &a = BLK == 64 ? *(const PipeArgs *)__builtin_amdgcn_kernarg_segment_ptr() : a_arg;
+#elif defined(__HIP_DEVICE_COMPILE__)
     const PipeArgs &a = *(const PipeArgs *)__builtin_amdgcn_kernarg_segment_ptr();
 #else
     const PipeArgs &a = a_arg;  // the host pass only type-checks the body
