@@ -751,7 +751,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
                 ofill = 0;
                 opend = 0;
             }
-            ck_b = STAT_CLK(); ck_fwd += ck_b - ck_a; ck_a = ck_b;
+            if (STAT_ON) { ck_b = STAT_GCLK(); ck_fwd += ck_b ? ck_b - ck_a : 0; }  // FINE builds only
             continue;
         }
         if (!has_out) {
