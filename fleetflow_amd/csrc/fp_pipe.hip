@@ -344,10 +344,9 @@ template <uint32_t G, uint32_t BLK>
 __global__ __launch_bounds__(BLK, BLK == 64 ? (G == 12 ? WIDE12_WAVES : WIDE_WAVES) : 1) void
 k_ffd_pipe(const PipeArgs a_arg) {
     // the arguments are read through the kernarg segment (memory), not promoted to SGPRs for the
-    // whole kernel: held in SGPRs they spilled into VGPR lanes (781 v_readlane vs 296)
-#if defined(__HIP_DEVICE_COMPILE__) && defined(FP_AB_NARROW_BYVAL)
-    const PipeArgs &a = BLK == 64 ? *(const PipeArgs *)__builtin_amdgcn_kernarg_segment_ptr() : a_arg;
-#elif defined(__HIP_DEVICE_COMPILE__)
+    // whole kernel: held in SGPRs they spilled into VGPR lanes (wide kernel: 781 v_readlane vs 296,
+    // config-4 FFD 16.7 vs 15.2 ms; narrow kernel by value: config 3 65.9 vs 65.0 ms, r04o A/B)
+#if defined(__HIP_DEVICE_COMPILE__)
     const PipeArgs &a = *(const PipeArgs *)__builtin_amdgcn_kernarg_segment_ptr();
 #else
     const PipeArgs &a = a_arg;  // the host pass only type-checks the body
