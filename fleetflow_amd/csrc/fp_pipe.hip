@@ -42,13 +42,16 @@ __device__ unsigned long long g_pipe_stats[16 * 16];
 #define STAT_ADD(w, i, v) atomicAdd(&g_pipe_stats[(w) * 16 + (i)], (unsigned long long)(v))
 #define STAT_CLK() __builtin_amdgcn_s_memtime()
 #define STAT_ON 1
-// per group-queue timers ([6] check loop, [7] mask upkeep cycles): two more s_memtime per queue,
-// which doubles config 3's diagnostics time, so only with FP_PIPE_STATS_FINE
+// per group-queue timers ([6] check loop, [7] mask upkeep cycles, [14] queues, [15] touched nodes)
+// and the global-link forwarding timer: they doubled config 3's diagnostics time, so only with
+// FP_PIPE_STATS_FINE
 // (tools/build_variant.sh _statsfine -DFP_PIPE_STATS -DFP_PIPE_STATS_FINE)
 #ifdef FP_PIPE_STATS_FINE
 #define STAT_GCLK() __builtin_amdgcn_s_memtime()
+#define STAT_FINE 1
 #else
 #define STAT_GCLK() 0ull
+#define STAT_FINE 0
 #endif
 // per-batch timeline of scenario 0: [stage][batch] = (t_in_ready, t_prescan, t_cand, t_out_done)
 constexpr int TL_B = 2048;
@@ -63,6 +66,7 @@ __device__ unsigned long long g_stage_span[SPAN_MAX * 8];
 #define STAT_CLK() 0ull
 #define STAT_GCLK() 0ull
 #define STAT_ON 0
+#define STAT_FINE 0
 #endif
 
 namespace fpp {
@@ -297,7 +301,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                     fpp_group_x<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                        req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
                 const unsigned long long gc1 = STAT_GCLK();
-                if (STAT_ON) { gst[0] += gc1 - gc0; gst[2] += 1; gst[3] += (uint32_t)__builtin_popcountll(touched); }
+                if (STAT_FINE) { gst[0] += gc1 - gc0; gst[2] += 1; gst[3] += (uint32_t)__builtin_popcountll(touched); }
                 if (touched) {
                     const bool me = (touched >> lane) & 1ull;
                     if (gs < 32) used |= me ? (1u << gs) : 0u;
@@ -319,7 +323,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                                       ~clr);
                     }
                 }
-                if (STAT_ON) gst[1] += STAT_GCLK() - gc1;
+                if (STAT_FINE) gst[1] += STAT_GCLK() - gc1;
             }
         }(),
         ...);
@@ -675,10 +679,8 @@ k_ffd_pipe(const PipeArgs a_arg) {
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
                                        __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
-            if (STAT_ON) {
-                st_checks += nchk; st_hits += nhit;
-                ck_gx += gst[0]; ck_gu += gst[1]; st_queues += (uint32_t)gst[2]; st_touched += (uint32_t)gst[3];
-            }
+            if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
+            if (STAT_FINE) { ck_gx += gst[0]; ck_gu += gst[1]; st_queues += (uint32_t)gst[2]; st_touched += (uint32_t)gst[3]; }
         }
         if (zs_g < G) {
             // all-zero containers change no record: each takes the first schedulable node
@@ -750,7 +752,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
                 ofill = 0;
                 opend = 0;
             }
-            if (STAT_ON) { ck_b = STAT_GCLK(); ck_fwd += ck_b ? ck_b - ck_a : 0; }  // FINE builds only
+            if (STAT_FINE) { ck_b = STAT_GCLK(); ck_fwd += ck_b - ck_a; }
             continue;
         }
         if (!has_out) {
@@ -1296,8 +1298,11 @@ bool fp_pipe_plan(const fp_ctx *c, uint32_t S, uint32_t N, uint32_t *G_out, uint
     // groups) 7 segments of 12 groups 28.3 ms, 10 of 8 groups 28.2, 4 of 20 groups 30.3,
     // 3 of 24-28 groups 30.2.  (Without the lag, when a segment waited on its upstream
     // half its life, 4 segments of 20 groups were best: 56.7 ms vs 64.1 for 5 of 16.)
+    // Round 4 (r04p / r04q sweeps of config 4's per-GPU loads): 8-group segments are faster at up to
+    // 1024 scenarios (1024: 8.47 vs 8.73 ms, 512: 7.42 vs 7.51) and 12 above (2048: 9.91 vs 10.19,
+    // 4096: 15.17 vs 18.9 with 16 groups) -- the strong-scaled ranks of the 8-GPU run hold 512-1024.
     const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg
-                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : 12u;
+                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : S <= 1024 ? 8u : 12u;
     const uint32_t B = (NG + seg_groups - 1) / seg_groups;
     const uint32_t per_seg = (NG + B - 1) / B;
     const uint32_t first_w = forced_w > 0 ? (uint32_t)forced_w : narrow ? 4u : 1u;

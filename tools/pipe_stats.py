@@ -50,7 +50,7 @@ def main():
             continue
         b = max(v[3], 1)
         print(f"{w:5d} {v[0]/S:12.0f} {v[1]/S:12.0f} {v[2]/S:10.0f} {v[3]/S:13.0f} {v[4]/b:14.1f} {v[5]/b:15.1f}")
-    print("stage  Mcycles/scen: input  prescan  cand_loop  fwd  out_wait  total   | cycles/check  (checks / mask upkeep: FP_PIPE_STATS_FINE builds)")
+    print("stage  Mcycles/scen: input  prescan  cand_loop  fwd  out_wait  total   | cycles/check  (checks / mask upkeep / queues / touched: FP_PIPE_STATS_FINE builds)")
     for w in range(16):
         v = [buf[w * 16 + i] for i in range(16)]
         if not any(v):

@@ -21,7 +21,7 @@ from fleetflow_amd._lib import FP_K_PLACE  # noqa: E402
 
 LOADS = {"c3": (1, 1_000_000, 100_000, 0x5EED0003), "c2": (1, 10_000, 1_000, 0x5EED0002),
          "c4x512": (512, 50_000, 5_000, 0x5EED0004), "c4x1024": (1024, 50_000, 5_000, 0x5EED0004),
-         "c4x4096": (4096, 50_000, 5_000, 0x5EED0004)}
+         "c4x2048": (2048, 50_000, 5_000, 0x5EED0004), "c4x4096": (4096, 50_000, 5_000, 0x5EED0004)}
 
 
 def main():
