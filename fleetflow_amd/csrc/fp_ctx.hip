@@ -70,6 +70,9 @@ extern "C" void fp_ctx_destroy(fp_ctx *c) {
     if (c->last_ev) (void)hipEventDestroy(c->last_ev);
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->h_in_ev) (void)hipEventSynchronize(c->h_in_ev);
+    if (c->h_in) (void)hipHostFree(c->h_in);
+    if (c->h_in_ev) (void)hipEventDestroy(c->h_in_ev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -312,16 +315,98 @@ static int copy_back_all(fp_ctx *c, const OutCopy *o, int n) {
     return FP_OK;
 }
 
+// Small host-pointer calls (a fleet.kdl stage: config 1) pay per HIP call, not per byte: the
+// inputs go through one pinned buffer and ONE host-to-device copy, and the results plus the
+// call's error word come back in ONE device-to-host copy of the contiguous staging span
+// (6 HIP calls per fp_levelize instead of 10; the results are still written only when the error
+// word is clean).
+struct InCopy {
+    const void *h;
+    size_t bytes;
+    const void **d;  // receives the device copy (nullptr when h is null)
+};
+static int stage_in_packed(fp_ctx *c, const InCopy *in, int n) {
+    size_t total = 0;
+    for (int i = 0; i < n; ++i)
+        if (in[i].h) total += align256(in[i].bytes + 4);
+    if (!total) {
+        for (int i = 0; i < n; ++i) *in[i].d = nullptr;
+        return FP_OK;
+    }
+    if (c->h_in_ev) FP_HIP(hipEventSynchronize(c->h_in_ev));  // the previous copy out of h_in is done
+    if (total > c->h_in_cap) {
+        if (c->h_in) (void)hipHostFree(c->h_in);
+        c->h_in = nullptr;
+        c->h_in_cap = 0;
+        const size_t cap = align256(total + total / 4 + 4096);
+        FP_HIP(hipHostMalloc(&c->h_in, cap, hipHostMallocDefault));
+        c->h_in_cap = cap;
+    }
+    if (!c->h_in_ev) FP_HIP(hipEventCreateWithFlags(&c->h_in_ev, hipEventDisableTiming));
+    char *d = (char *)fp_stage_take(c, total);
+    if (!d) return FP_ENOMEM;
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!in[i].h) { *in[i].d = nullptr; continue; }
+        memcpy(c->h_in + off, in[i].h, in[i].bytes);
+        *in[i].d = d + off;
+        off += align256(in[i].bytes + 4);
+    }
+    FP_HIP(hipMemcpyAsync(d, c->h_in, total, hipMemcpyHostToDevice, c->stream));
+    FP_HIP(hipEventRecord(c->h_in_ev, c->stream));
+    return FP_OK;
+}
+// Results from stage_out buffers taken one after another (a contiguous span of the staging
+// arena): the call's error word is copied behind them on the device, the span comes back in one
+// copy, and the caller's buffers are written only when that word is clean.
+static int copy_back_span(fp_ctx *c, const OutCopy *o, int n) {
+    const char *lo = nullptr, *hi = nullptr;
+    for (int i = 0; i < n; ++i) {
+        if (!o[i].d) continue;
+        const char *a = (const char *)o[i].d, *b = a + o[i].bytes;
+        if (!lo || a < lo) lo = a;
+        if (!hi || b > hi) hi = b;
+    }
+    uint32_t *slot = (uint32_t *)fp_stage_take(c, 4);
+    if (!slot) return FP_ENOMEM;
+    if (!lo) lo = (const char *)slot;
+    if ((const char *)slot < hi) return FP_EINVAL;  // not the layout this helper assumes
+    const size_t span = (size_t)((const char *)slot + 4 - lo);
+    if (span > c->h_stage_cap) {
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_cap = 0;
+        const size_t cap = align256(span + span / 4 + 4096);
+        FP_HIP(hipHostMalloc(&c->h_stage, cap, hipHostMallocDefault));
+        c->h_stage_cap = cap;
+    }
+    FP_HIP(hipMemcpyAsync(slot, c->d_err, 4, hipMemcpyDeviceToDevice, c->stream));
+    FP_HIP(hipMemcpyAsync(c->h_stage, lo, span, hipMemcpyDeviceToHost, c->stream));
+    FP_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t e = *(const uint32_t *)(c->h_stage + ((const char *)slot - lo));
+    if (e) {
+        FP_HIP(hipMemsetAsync(c->d_err, 0, 4, c->stream));
+        FP_HIP(hipStreamSynchronize(c->stream));
+        return -(int)e;
+    }
+    for (int i = 0; i < n; ++i)
+        if (o[i].h && o[i].bytes) memcpy(o[i].h, c->h_stage + ((const char *)o[i].d - lo), o[i].bytes);
+    return FP_OK;
+}
+
 extern "C" int fp_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm_out) {
     if (!c || !g || (g->n_vertices && (!g->has_deps || !perm_out))) return FP_EINVAL;
     fp_host_err_scope es(c);
     FP_HIP(hipSetDevice(c->device));
     const size_t V = g->n_vertices;
-    int rc = fp_stage_reserve(c, 2 * V * 4 + 4096);
+    int rc = fp_stage_reserve(c, 2 * V * 4 + 8192);
     if (rc) return rc;
     fp_stage_reset(c);
     fp_graph dg = *g;
-    dg.has_deps = stage_in(c, g->has_deps, V, &rc);
+    const void *dhd = nullptr;
+    const InCopy in[] = {{g->has_deps, V, &dhd}};
+    if ((rc = stage_in_packed(c, in, 1))) return rc;
+    dg.has_deps = (const uint8_t *)dhd;
     dg.row_ptr = nullptr;
     dg.col = nullptr;
     uint32_t *dperm = stage_out<uint32_t>(c, V, &rc);
@@ -329,7 +414,7 @@ extern "C" int fp_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm_out)
     rc = fp_dev_legacy_order_impl(c, &dg, dperm);
     if (rc) return rc;
     const OutCopy o[] = {{perm_out, dperm, V * 4}};
-    return copy_back_all(c, o, 1);
+    return copy_back_span(c, o, 1);
 }
 
 extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, uint32_t *order_out,
@@ -346,13 +431,17 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
     // the CSR is validated on the device (k_check_csr, k_indeg): FP_ECORRUPT
     FP_HIP(hipSetDevice(c->device));
     fp_host_err_scope es(c);
-    int rc = fp_stage_reserve(c, (V + 1) * 4 + E * 4 + V + 2 * V * 4 + 8 * 256);
+    int rc = fp_stage_reserve(c, (V + 1) * 4 + E * 4 + V + 2 * V * 4 + 16 * 256);
     if (rc) return rc;
     fp_stage_reset(c);
     fp_graph dg = *g;
-    dg.row_ptr = stage_in(c, g->row_ptr, V + 1, &rc);
-    dg.col = stage_in(c, g->col, E, &rc);
-    dg.has_deps = stage_in(c, g->has_deps, V, &rc);
+    const void *drp = nullptr, *dcol = nullptr, *dhd = nullptr;
+    const InCopy in[] = {{g->row_ptr, (V + 1) * 4, &drp}, {E ? g->col : nullptr, E * 4, &dcol},
+                         {g->has_deps, V, &dhd}};
+    if ((rc = stage_in_packed(c, in, 3))) return rc;
+    dg.row_ptr = (const uint32_t *)drp;
+    dg.col = (const uint32_t *)dcol;
+    dg.has_deps = (const uint8_t *)dhd;
     uint32_t *dlev = stage_out<uint32_t>(c, V, &rc);
     uint32_t *dord = stage_out<uint32_t>(c, V, &rc);
     uint32_t *dcyc = stage_out<uint32_t>(c, 1, &rc);
@@ -360,7 +449,7 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
     rc = fp_dev_levelize_impl(c, &dg, dlev, dord, dcyc);
     if (rc) return rc;
     const OutCopy o[] = {{level_out, dlev, V * 4}, {order_out, dord, V * 4}, {n_cycle_out, dcyc, 4}};
-    return copy_back_all(c, o, 3);
+    return copy_back_span(c, o, 3);
 }
 
 static int batch_host(fp_ctx *c, const fp_batch *b) {

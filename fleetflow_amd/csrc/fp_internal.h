@@ -45,6 +45,11 @@ struct fp_ctx {
     // kernel and every device-to-host copy succeeded (all-or-nothing)
     char *h_stage = nullptr;
     size_t h_stage_cap = 0;
+    // pinned host staging of host-API inputs (one host-to-device copy per call); h_in_ev marks the
+    // last copy out of it, waited on before the buffer is written again
+    char *h_in = nullptr;
+    size_t h_in_cap = 0;
+    hipEvent_t h_in_ev = nullptr;
     // profiling
     bool profile = false;
     struct Rec { int kid; hipEvent_t a, b; };
