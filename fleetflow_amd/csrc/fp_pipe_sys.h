@@ -28,9 +28,10 @@
 namespace fpp {
 
 #ifdef FP_PIPE_STATS
-// systolic-call diagnostics (stats build): [0] calls [1] queued Q [2] live L [3] steps [4] placed
-// [5] live nodes that fit at least one queued container (2-D + labels/conflicts, batch-start state)
-// [6] largest placement position + 1, summed over calls
+// systolic-call diagnostics (FP_PIPE_STATS_FINE builds, tools/sys_stats.py): [0] calls [1] queued Q
+// [2] live L [3] steps [4] placed [5] live nodes that fit at least one queued container (2-D +
+// labels/conflicts, batch-start state) [6] largest placement position + 1, summed over calls.  A
+// loop over the queue and seven atomics per call: they doubled config 3's plain diagnostics time
 __device__ unsigned long long g_sys_stats[8];
 #endif
 
@@ -176,7 +177,7 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     uint32_t tau = 0;                                         // steps taken = rotations applied
     uint32_t apos = 0xFFFFFFFFu;                              // step of the placement (compacted lane)
     fpp_sys_steps(xc, xm, xu, xl, kc, km, kr, kx, apos, pend, tau, L, max_steps);
-#ifdef FP_PIPE_STATS
+#if defined(FP_PIPE_STATS) && defined(FP_PIPE_STATS_FINE)
     {
         // live nodes some queued container fits at the batch-start state (before the steps: the
         // records below are still the node lanes' own)

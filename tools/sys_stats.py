@@ -1,7 +1,8 @@
 """Diagnostics: systolic group-fill calls on one workload (stats build): calls, queued containers,
 live nodes, steps, placements, live nodes some queued container fits, last placement position.
 
-    FLEETPLACE_LIB=$PWD/fleetflow_amd/libfleetplace_stats.so python tools/sys_stats.py [S C N seed]
+    tools/build_variant.sh _statsfine -DFP_PIPE_STATS -DFP_PIPE_STATS_FINE
+    FLEETPLACE_LIB=$PWD/fleetflow_amd/libfleetplace_statsfine.so python tools/sys_stats.py [S C N seed]
 """
 import ctypes as ct
 import json
