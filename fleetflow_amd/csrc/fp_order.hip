@@ -1014,7 +1014,11 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
                 FP_HIP(hipGetLastError());
             }
             // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
-            k_lvl_async<<<512, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err, pk, bad);
+#ifndef FP_LVL_GRID
+#define FP_LVL_GRID 512
+#endif
+            k_lvl_async<<<FP_LVL_GRID, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err, pk,
+                                                    bad);
             FP_HIP(hipGetLastError());
         }
         // the cycle key (from the largest level seen) is computed on the device: no read-back
