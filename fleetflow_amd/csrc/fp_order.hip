@@ -199,6 +199,11 @@ constexpr uint32_t kLaneEdges = 1;        // edges a lane relaxes per round
 // 0.92 -- more records to build and load per round, profiles/r04m_lvl_hops_ab.txt)
 constexpr uint32_t kHops = 4;
 constexpr uint32_t kPush = kLaneEdges + kHops;  // queue entries a lane may push per round
+// one-wave blocks of the persistent grid: 8 waves per CU (config 5: 2048 0.78 ms, 512 0.84, 4096 0.79,
+// 8192 0.81, 256 0.92; profiles/r04v_lvl_grid_ab.txt) -- a wave round lasts as long as its slowest
+// lane, so spreading the items over more waves shortens the rounds of the lanes on the long chains,
+// until idle waves' queue polls start to cost more
+constexpr uint32_t kAsyncBlocks = 2048;
 // ctl layout (u32 index): head[s] = s*32, tail[s] = (8+s)*32, done[s] = (16+s)*32,
 // fin = 24*32, abort = 25*32, maxlvl = 26*32
 constexpr uint32_t kCtlWords = 27 * kCtlStride;
@@ -980,7 +985,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_LEVEL, &ev);
     FP_HIP(hipMemsetAsync(indeg, 0, (size_t)V * 4, st));
-    FP_HIP(hipMemsetAsync(cnt, 0, ncnt * 4, st));
+    if (level_sync) FP_HIP(hipMemsetAsync(cnt, 0, ncnt * 4, st));  // the per-level frontier counts
     FP_HIP(hipMemsetAsync(ncyc, 0, 64, st));
     k_check_csr<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, V, E, c->d_err, bad);
     FP_HIP(hipGetLastError());
@@ -1013,12 +1018,9 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
                                                bad);
                 FP_HIP(hipGetLastError());
             }
-            // one wave per block, two per CU: enough lanes for a 10k-vertex frontier
-#ifndef FP_LVL_GRID
-#define FP_LVL_GRID 512
-#endif
-            k_lvl_async<<<FP_LVL_GRID, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err, pk,
-                                                    bad);
+            // one wave per block, kAsyncBlocks of them
+            k_lvl_async<<<kAsyncBlocks, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err,
+                                                     pk, bad);
             FP_HIP(hipGetLastError());
         }
         // the cycle key (from the largest level seen) is computed on the device: no read-back
