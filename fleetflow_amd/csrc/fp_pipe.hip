@@ -336,7 +336,10 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
 // SIMD: 5 fits them in 96 VGPRs (32 B of scratch) and 20 segments per CU -- config-4 FFD 20.9 ->
 // 18.7 ms against the 1024-thread kernel's 107 VGPRs and four waves (6 waves: 80 VGPRs, 100 B of
 // scratch, 19.2 ms).
-constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
+#ifndef FP_WIDE12_WAVES
+#define FP_WIDE12_WAVES 5
+#endif
+constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = FP_WIDE12_WAVES;
 // Batch prescan: a group with an empty batch corner skips its bucket-mask loads in the wide stages
 // (config-4 FFD 17.38 -> 15.72 ms: a batch that passes a segment mostly has every corner empty);
 // the narrow stages keep the branch-free form (config 3: 64.3 vs 65.3 ms with the skip; r03z A/B,
