@@ -336,10 +336,12 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
 // SIMD: 5 fits them in 96 VGPRs (32 B of scratch) and 20 segments per CU -- config-4 FFD 20.9 ->
 // 18.7 ms against the 1024-thread kernel's 107 VGPRs and four waves (6 waves: 80 VGPRs, 100 B of
 // scratch, 19.2 ms).
-#ifndef FP_WIDE12_WAVES
-#define FP_WIDE12_WAVES 5
-#endif
-constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = FP_WIDE12_WAVES;
+constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
+// Batches of at least WIDE12_BIG_S scenarios use a second 12-group instantiation compiled for six
+// waves per SIMD (80 VGPRs, 84 B of scratch, 6144 resident segments): config 4 at 4096 scenarios
+// FFD 14.93-14.95 vs 15.20-15.23 ms; at 2048 it loses (10.21-10.35 vs 9.87-9.90), the spills costing
+// more than the extra slots buy (profiles/r04x_waves_ab.jsonl)
+constexpr uint32_t WIDE12_BIG_WAVES = 6, WIDE12_BIG_S = 4096;
 // Batch prescan: a group with an empty batch corner skips its bucket-mask loads in the wide stages
 // (config-4 FFD 17.38 -> 15.72 ms: a batch that passes a segment mostly has every corner empty);
 // the narrow stages keep the branch-free form (config 3: 64.3 vs 65.3 ms with the skip; r03z A/B,
@@ -347,8 +349,8 @@ constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = FP_WIDE12_WAVES;
 // FFD 15.62 -> 15.06 ms, config 3 64.3 -> 63.6 ms; r03aa/r03ab).  Measured slower and removed in
 // round 4: per-group capacity bounds in place of the corner ballots (15.73 vs 15.08
 // ms, r03af), req / conf of link input loaded after the prescan (15.45 vs 15.08 ms, r03ac).
-template <uint32_t G, uint32_t BLK>
-__global__ __launch_bounds__(BLK, BLK == 64 ? (G == 12 ? WIDE12_WAVES : WIDE_WAVES) : 1) void
+template <uint32_t G, uint32_t BLK, uint32_t WV = 0>
+__global__ __launch_bounds__(BLK, BLK == 64 ? (WV ? WV : G == 12 ? WIDE12_WAVES : WIDE_WAVES) : 1) void
 k_ffd_pipe(const PipeArgs a_arg) {
     // the arguments are read through the kernarg segment (memory), not promoted to SGPRs for the
     // whole kernel: held in SGPRs they spilled into VGPR lanes (wide kernel: 781 v_readlane vs 296,
@@ -1224,12 +1226,12 @@ size_t lds_bytes(uint32_t W, uint32_t G, uint32_t R) {
 }
 
 // G is a template parameter (records are register arrays); one instantiation per G
-template <uint32_t G, uint32_t BLK = 1024>
+template <uint32_t G, uint32_t BLK = 1024, uint32_t WV = 0>
 static int launch_g(hipStream_t st, unsigned grid, unsigned block, size_t lds, const PipeArgs &a) {
     if (block > BLK) return FP_EINVAL;
-    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe<G, BLK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe<G, BLK, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    k_ffd_pipe<G, BLK><<<grid, block, lds, st>>>(a);
+    k_ffd_pipe<G, BLK, WV><<<grid, block, lds, st>>>(a);
     return FP_OK;
 }
 
@@ -1258,6 +1260,10 @@ static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {
     (const void *)k_ffd_pipe<24, 64>, (const void *)k_ffd_pipe<28, 64>, (const void *)k_ffd_pipe<32, 64>,
     (const void *)k_ffd_pipe<36, 64>, (const void *)k_ffd_pipe<40, 64>};
 static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G >= 12; }
+// the six-wave 12-group instantiation (WIDE12_BIG_S)
+static const launch_fn kLaunchWide12Big = launch_g<12, 64, WIDE12_BIG_WAVES>;
+static const void *const kKernelWide12Big = (const void *)k_ffd_pipe<12, 64, WIDE12_BIG_WAVES>;
+static inline bool wide12_big(uint32_t S, uint32_t W, uint32_t G) { return W == 1 && G == 12 && S >= WIDE12_BIG_S; }
 
 }  // namespace fpp
 
@@ -1365,8 +1371,9 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
         int dev_cu = 0, occ = 0;
         (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
         const bool wide = wide_g(W, G);
-        const void *fn = wide ? (G / 4 < sizeof(kKernelWide) / sizeof(kKernelWide[0]) ? kKernelWide[G / 4] : nullptr)
-                              : (G < sizeof(kKernel) / sizeof(kKernel[0]) ? kKernel[G] : nullptr);
+        const void *fn = wide12_big(S, W, G) ? kKernelWide12Big
+                         : wide ? (G / 4 < sizeof(kKernelWide) / sizeof(kKernelWide[0]) ? kKernelWide[G / 4] : nullptr)
+                                : (G < sizeof(kKernel) / sizeof(kKernel[0]) ? kKernel[G] : nullptr);
         if (fn && dev_cu > 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), g->lds) == hipSuccess && occ > 0)
             slots_total = (uint64_t)occ * (uint64_t)dev_cu;
     }
@@ -1536,7 +1543,8 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     if (G < 1 || (wide ? (G > MAX_G_WIDE || G % 4) : G > MAX_G)) return FP_EOVERFLOW;
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
-    int rc = (wide ? kLaunchWide[G / 4] : kLaunch[G])(st, (unsigned)(S * B), W * 64, lds, a);
+    int rc = (wide12_big(S, W, G) ? kLaunchWide12Big : wide ? kLaunchWide[G / 4] : kLaunch[G])(st, (unsigned)(S * B),
+                                                                                               W * 64, lds, a);
     if (rc) return rc;
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
