@@ -116,7 +116,7 @@ def test_forced_bounded_links_without_residency_fail_promptly(planner, opts):
     from fleetflow_amd import DevBatch
     from fleetflow_amd._lib import FP_EDEVICE, FleetplaceError
     C, N = 12_000, 5_000  # 7 segments of 12 groups; segment 0 (768 nodes) forwards ~4k per scenario
-    S = planner.geometry(1024, C, N)["resident"] + 256
+    S = planner.geometry(8192, C, N)["resident"] + 256  # the resident slots of a batch this large
     db = DevBatch.allocate(S, C, N, "cuda:0")
     planner.dev_gen_batch(0x5EED0004, db, 7)
     snap = db.node_snapshot()
