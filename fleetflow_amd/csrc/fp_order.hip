@@ -193,8 +193,11 @@ __global__ void k_lvl_final(const uint32_t *__restrict__ indeg, uint32_t V, uint
 constexpr uint32_t kShards = 8;           // queues (blocks b and b+8 share an XCD)
 constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B lines)
 constexpr uint64_t kQEmpty = ~0ull;
-constexpr uint32_t kCoopEdges = 16;       // edges left at which the wave expands a vertex together
-constexpr uint32_t kLaneEdges = 1;        // edges a lane relaxes per round
+// edges left at which the wave expands a vertex together, and edges a lane relaxes per round
+// (config 5: 16 / 1 0.775 ms; cooperative at 8 0.823, at 32 0.779; 2 edges per lane 0.877;
+// profiles/r04aa_lvl_tuning_ab.txt)
+constexpr uint32_t kCoopEdges = 16;
+constexpr uint32_t kLaneEdges = 1;
 // levels a lane may jump per round along only-parent first edges: 4 (config 5 0.84 ms; 6 hops 0.86, 8 hops
 // 0.92 -- more records to build and load per round, profiles/r04m_lvl_hops_ab.txt)
 constexpr uint32_t kHops = 4;
