@@ -340,7 +340,9 @@ constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
 // Batches of at least WIDE12_BIG_S scenarios use a second 12-group instantiation compiled for six
 // waves per SIMD (80 VGPRs, 84 B of scratch, 6144 resident segments): config 4 at 4096 scenarios
 // FFD 14.93-14.95 vs 15.20-15.23 ms; at 2048 it loses (10.21-10.35 vs 9.87-9.90), the spills costing
-// more than the extra slots buy (profiles/r04x_waves_ab.jsonl)
+// more than the extra slots buy (profiles/r04x_waves_ab.jsonl).  The 8-group segments of batches of up to
+// 1024 scenarios stay at five waves (k_ffd_pipe<8, 1024>, 82 VGPRs): six or seven waves ran 1024
+// scenarios 8.69 / 9.18 vs 8.46-8.54 ms (profiles/r04ab_small8_waves_ab.jsonl)
 constexpr uint32_t WIDE12_BIG_WAVES = 6, WIDE12_BIG_S = 4096;
 // Batch prescan: a group with an empty batch corner skips its bucket-mask loads in the wide stages
 // (config-4 FFD 17.38 -> 15.72 ms: a batch that passes a segment mostly has every corner empty);
