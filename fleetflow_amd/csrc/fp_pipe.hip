@@ -1309,14 +1309,18 @@ bool fp_pipe_plan(const fp_ctx *c, uint32_t S, uint32_t N, uint32_t *G_out, uint
     // groups) 7 segments of 12 groups 28.3 ms, 10 of 8 groups 28.2, 4 of 20 groups 30.3,
     // 3 of 24-28 groups 30.2.  (Without the lag, when a segment waited on its upstream
     // half its life, 4 segments of 20 groups were best: 56.7 ms vs 64.1 for 5 of 16.)
-    // Round 4 (r04p / r04q sweeps of config 4's per-GPU loads): 8-group segments are faster at up to
-    // 1024 scenarios (1024: 8.47 vs 8.73 ms, 512: 7.42 vs 7.51) and 12 above (2048: 9.91 vs 10.19,
-    // 4096: 15.17 vs 18.9 with 16 groups) -- the strong-scaled ranks of the 8-GPU run hold 512-1024.
+    // Round 4 (sweeps of config 4's per-GPU loads, profiles/r04p_*, r04q_*, r04ad_*): the strong-scaled
+    // ranks of the 8-GPU run hold 512-1024 scenarios, where a scenario's own chain sets the time and
+    // more stages per segment pay: up to 512 scenarios 2 segments of 4 stages x 10 groups (6.87 ms
+    // FFD vs 7.30 for one-wave 8-group segments, 7.51 for 12), up to 1024 5 segments of 2 stages x
+    // 8 groups (8.19 vs 8.46 and 8.73), above that one-wave 12-group segments (2048: 9.91 vs 10.19
+    // with 8 groups; 4096: 15.2 vs 18.9 with 16).
+    const bool mid4 = !narrow && S <= 512, mid2 = !narrow && !mid4 && S <= 1024;
     const uint32_t seg_groups = forced_seg > 0 && forced_seg <= (int)MAX_SEG_GROUPS ? (uint32_t)forced_seg
-                                : narrow ? 4u : forced_w > 1 ? MAX_SEG_GROUPS : S <= 1024 ? 8u : 12u;
+                                : narrow ? 4u : (forced_w > 1 || mid4) ? MAX_SEG_GROUPS : mid2 ? 16u : 12u;
     const uint32_t B = (NG + seg_groups - 1) / seg_groups;
     const uint32_t per_seg = (NG + B - 1) / B;
-    const uint32_t first_w = forced_w > 0 ? (uint32_t)forced_w : narrow ? 4u : 1u;
+    const uint32_t first_w = forced_w > 0 ? (uint32_t)forced_w : narrow ? 4u : mid4 ? 4u : mid2 ? 2u : 1u;
     // a forced stage count is tried first; sizes it cannot serve fall back to the list
     for (uint32_t W : {first_w, 4u, 8u, 2u, 1u, 12u, 16u}) {
         if (W > per_seg && W > 1) continue;

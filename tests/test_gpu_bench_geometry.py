@@ -96,13 +96,16 @@ def test_forced_lag_geometries(S, seg, publish, lag, planner, O, opts):
 def test_geometry_query_defaults(planner):
     """fp_place_geometry reports what the planner picks: configs 2/3 (one scenario, narrow
     segments of four one-group stages, lag 0), config 4's shape at 256 scenarios (fits at once:
-    lag 0; 8-group one-wave segments up to 1024 scenarios) and at 2048 (12-group segments)."""
+    lag 0; two segments of four 10-group stages up to 512 scenarios), at 1024 (five segments of
+    two 8-group stages) and at 2048 (one-wave 12-group segments)."""
     g3 = planner.geometry(1, 1_000_000, 100_000)
     assert (g3["groups"], g3["stages"], g3["lag"]) == (1, 4, 0) and g3["segments"] == 391, g3
     g2 = planner.geometry(1, 10_000, 1_000)
     assert g2["segments"] * g2["stages"] * g2["groups"] >= 16 and g2["lag"] == 0, g2
     g4 = planner.geometry(256, 50_000, 5_000)
-    assert g4["lag"] == 0 and (g4["groups"], g4["stages"], g4["segments"]) == (8, 1, 10), g4
+    assert g4["lag"] == 0 and (g4["groups"], g4["stages"], g4["segments"]) == (10, 4, 2), g4
+    g4m = planner.geometry(1024, 50_000, 5_000)
+    assert (g4m["groups"], g4m["stages"], g4m["segments"]) == (8, 2, 5), g4m
     g4b = planner.geometry(2048, 50_000, 5_000)
     assert (g4b["groups"], g4b["stages"], g4b["segments"]) == (12, 1, 7), g4b
 
