@@ -1056,8 +1056,8 @@ __global__ void k_gather_sorted(const uint32_t *__restrict__ thr, uint32_t kpack
 // The rest of the sorted SoA after k_scen_sort (fp_place.hip) wrote order, cpu, mem and the
 // position word: req and conf gathered at random (same XCD-contiguous tiles as
 // k_gather_sorted, so an XCD's random lines stay in its L2) and the CYCLE bit from level.
-// (Interleaving req/conf in k_digits for one 8-byte read per container: gather 2.18 ->
-// 1.68 ms, but k_digits 0.39 -> 1.05 ms.)
+// (Interleaving req/conf in round 3's k_digits pass for one 8-byte read per container: gather
+// 2.18 -> 1.68 ms, but k_digits 0.39 -> 1.05 ms.)
 __global__ void k_gather_payload(uint32_t S, uint32_t C, const uint32_t *__restrict__ order,
                                  const uint32_t *__restrict__ req, const uint32_t *__restrict__ conf,
                                  const uint32_t *__restrict__ level, const uint32_t *__restrict__ summ,

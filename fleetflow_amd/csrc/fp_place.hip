@@ -230,7 +230,7 @@ __global__ void k_argmin_cost(const uint64_t *__restrict__ cost, uint32_t n, uin
 // A scenario without such digits takes the generic fallback (ss_generic) in the same workgroup.
 // Round 3 ranked against the whole batch's values instead: two streaming passes over every
 // container (k_value_bitmap, k_digits: 0.85 ms per 4096-scenario step) before the sort.
-// LDS: max(X u16[C], the rank tables' 96 KB) + ld u8[C] + [16][256] u16 + tables -> C <= ~50.3k.
+// LDS: max(X u16[C], the rank tables' 96 KB) + ld u8[C] + [16][256] u16 + tables -> C <= 50,336.
 constexpr uint32_t SS_DIG = 256;     // digits per dimension (dense ranks)
 constexpr uint32_t SS_WAVES = 16;
 constexpr uint32_t SS_CHUNKS = 50;   // 64-container chunks per wave slice: C <= 16 x 50 x 64 = 51,200

@@ -1,7 +1,7 @@
-"""GPU parity of the per-scenario LDS sort (fp_place.hip k_digits + k_scen_sort, fp_pipe.hip
-k_gather_payload): batches whose demands have at most 256 distinct values per dimension
-and scenarios of at most ~50.7k containers sort each scenario in one workgroup's LDS
-instead of the radix-key path.  Both paths must give the oracle's plan bit for bit; the
+"""GPU parity of the per-scenario LDS sort (fp_place.hip k_scen_sort, fp_pipe.hip k_payload_lds /
+k_gather_payload): scenarios of at most ~50.3k containers sort in one workgroup's LDS (digits
+from the scenario's own <= 256 distinct values per dimension, else the in-workgroup generic
+fallback) instead of the radix-key path.  Both paths must give the oracle's plan bit for bit; the
 cases push the kernel's limits (the LDS capacity, a single bucket holding every
 container, 256-value digits, equal keys in every wave, cycles)."""
 import zlib
@@ -12,9 +12,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 SEED = 0x5EED5050
-# largest C whose scenario fits the 160 KB of LDS: u16 index + u8 digit per container
-# (each array 16-B aligned) + 11,792 B of tables (fp_place.hip ss_lds_bytes)
-SS_MAX_C = 50_680
+# largest C whose scenario fits the 160 KB of LDS: u16 index (its region also holds the rank
+# tables, 96 KB) + u8 digit per container (each 16-B aligned) + 12,816 B of tables
+# (fp_place.hip ss_lds_bytes)
+SS_MAX_C = 50_336
 
 
 @pytest.fixture(params=["scen_sort", "scen_sort_gather", "radix"])
