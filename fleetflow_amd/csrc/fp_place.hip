@@ -254,6 +254,7 @@ struct ScenSortArgs {
     const uint32_t *cpu, *mem;               // [S][C] the demands
     uint32_t *order, *s_cpu, *s_mem, *s_idx; // [S][C] FFD order, sorted cpu / mem / position word
     const uint32_t *T;                       // [2 FP_BUCKETS] bucket thresholds (cpu, then mem; device)
+    const uint32_t *sbm, *scnt;              // the sample's presence bitmaps [2][RANK_WORDS] and counts (CN_*)
 };
 
 // the u16 digit rows are also counted, zeroed and scanned through 32/64-bit views: these
@@ -449,111 +450,137 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     const uint32_t *cpu = a.cpu + cb, *mem = a.mem + cb;
     const unsigned long long ck0 = SS_CLK();
 
-    // ---- R: the scenario's distinct values and dense ranks ----
-    for (uint32_t i = t; i < 2 * SR_W; i += blockDim.x) BMC[i] = 0u;
-    for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
-    if (t < 4) NEXT[t] = 0u;
-    __syncthreads();
-    {
-        bool big = false;
-        for (uint32_t k0 = 0; k0 < SS_CHUNKS; k0 += SS_LB) {  // coalesced, SS_LB x 2 loads in flight
+    // ---- R: the value set the digits rank against.  Pass 0 takes the sample's (k_value_bitmap
+    // over the first THR_SAMPLE scenarios: a 64-KB copy from L2) when it has <= 256 values per
+    // dimension; A0 then checks that every value of the scenario is in it, and a miss anywhere
+    // sends the workgroup to pass 1, the scenario's own distinct values (one streaming pass).  The
+    // digits are ranks in either set, so the order is exact either way. ----
+    const uint32_t scd = a.scnt[CN_DC], scm = a.scnt[CN_DM];
+    const bool samp = a.scnt[CN_OVER] == 0u && scd - 1u < SS_DIG && scm - 1u < SS_DIG;  // grid-uniform
+    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
+    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
+    uint16_t *myrow = WH + w * SS_DIG;
+    uint32_t dc = 0, dm = 0, hbits = 0, lbits = 0;
+    uint32_t dvp[SS_CHUNKS / 2];
+    unsigned long long ck1 = 0;
+    // one pass (inlined twice): 0 = ranked, 1 = a miss (pass 0 only), 2 = the generic sort ran
+    auto rank_pass = [&](const uint32_t pass) -> uint32_t {
+        for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
+        if (t < 4) NEXT[t] = 0u;
+        if (pass == 0) {
+            for (uint32_t i = t; i < 2 * SR_W; i += blockDim.x) BMC[i] = a.sbm[i];
+        } else {
+            for (uint32_t i = t; i < 2 * SR_W; i += blockDim.x) BMC[i] = 0u;
+            __syncthreads();
+            bool big = false;
+            for (uint32_t k0 = 0; k0 < SS_CHUNKS; k0 += SS_LB) {  // coalesced, SS_LB x 2 loads in flight
+                uint32_t cv[SS_LB], mv[SS_LB];
+#pragma unroll
+                for (uint32_t k = 0; k < SS_LB; ++k) {
+                    const uint32_t i = t + blockDim.x * (k0 + k);
+                    cv[k] = i < C ? __builtin_nontemporal_load(&cpu[i]) : 0u;
+                    mv[k] = i < C ? __builtin_nontemporal_load(&mem[i]) : 0u;
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < SS_LB; ++k) {
+                    if (t + blockDim.x * (k0 + k) < C) {
+                        const uint32_t c = cv[k], m = mv[k];
+                        if ((c | m) >= RANK_MAX_VALUE) {
+                            big = true;
+                        } else {  // test before set: most bits are already there
+                            const uint32_t bc = 1u << (c & 31), bm = 1u << (m & 31);
+                            if (!(BMC[c >> 5] & bc)) atomicOr(&BMC[c >> 5], bc);
+                            if (!(BMM[m >> 5] & bm)) atomicOr(&BMM[m >> 5], bm);
+                        }
+                    }
+                }
+            }
+            if (__ballot(big) && lane == 0) atomicOr(&NEXT[1], 1u);
+        }
+        __syncthreads();
+        // prefix popcounts: thread t owns words [8t, 8t + 8) of both bitmaps (SR_W = 8 x 1024)
+        static_assert(SR_W == 8 * 1024, "rank words per thread");
+        uint32_t bw[8], bx[8], sc = 0, sm = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            bw[j] = BMC[8 * t + j];
+            bx[j] = BMM[8 * t + j];
+            sc += (uint32_t)__popc(bw[j]);
+            sm += (uint32_t)__popc(bx[j]);
+        }
+        uint32_t pc = ss_block_excl(sc, HS, lane, w, dc);
+        __syncthreads();  // HS reused by the second scan
+        uint32_t pm = ss_block_excl(sm, HB, lane, w, dm);
+        const bool elig = NEXT[1] == 0u && dc >= 1u && dm >= 1u && dc <= SS_DIG && dm <= SS_DIG;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            PRC[8 * t + j] = (uint16_t)pc;
+            PRM[8 * t + j] = (uint16_t)pm;
+            if (elig) {  // the value of every rank, flipped to digit order (<= 256 bits in all)
+                for (uint32_t x = bw[j]; x; x &= x - 1) CV[dc - 1u - pc++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
+                for (uint32_t x = bx[j]; x; x &= x - 1) MV[dm - 1u - pm++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
+            } else {
+                pc += (uint32_t)__popc(bw[j]);
+                pm += (uint32_t)__popc(bx[j]);
+            }
+        }
+        __syncthreads();
+        if (!elig) {  // more than 256 distinct values in a dimension, or a value >= 2^18 (uniform)
+            ss_generic(a, X, WH, HS, HB, cb, C);
+            return 2u;
+        }
+        if (t < SS_DIG) {
+            MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, MV[t]) : 0;
+            CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, CV[t]) : 0;
+        }
+        ck1 = SS_CLK();
+        // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
+        hbits = dc > 1 ? 32u - (uint32_t)__builtin_clz(dc - 1u) : 0u;
+        lbits = dm > 1 ? 32u - (uint32_t)__builtin_clz(dm - 1u) : 0u;
+
+        // ---- A0: the wave's slice [s0, s1) ranked into digit pairs (kept in registers, two per
+        // dword), ld into LDS, per-wave hd counts; a value outside the set (pass 0) is a miss ----
+        bool miss = false;
+#pragma unroll
+        for (uint32_t k = 0; k < SS_CHUNKS / 2; ++k) dvp[k] = 0u;
+#pragma unroll
+        for (uint32_t k0 = 0; k0 < SS_CHUNKS; k0 += SS_LB) {
             uint32_t cv[SS_LB], mv[SS_LB];
 #pragma unroll
             for (uint32_t k = 0; k < SS_LB; ++k) {
-                const uint32_t i = t + blockDim.x * (k0 + k);
-                cv[k] = i < C ? __builtin_nontemporal_load(&cpu[i]) : 0u;
-                mv[k] = i < C ? __builtin_nontemporal_load(&mem[i]) : 0u;
+                const uint32_t p = s0 + 64 * (k0 + k) + lane;
+                cv[k] = p < s1 ? __builtin_nontemporal_load(&cpu[p]) : 0u;
+                mv[k] = p < s1 ? __builtin_nontemporal_load(&mem[p]) : 0u;
             }
 #pragma unroll
             for (uint32_t k = 0; k < SS_LB; ++k) {
-                if (t + blockDim.x * (k0 + k) < C) {
-                    const uint32_t c = cv[k], m = mv[k];
-                    if ((c | m) >= RANK_MAX_VALUE) {
-                        big = true;
-                    } else {  // test before set: most bits are already there
-                        const uint32_t bc = 1u << (c & 31), bm = 1u << (m & 31);
-                        if (!(BMC[c >> 5] & bc)) atomicOr(&BMC[c >> 5], bc);
-                        if (!(BMM[m >> 5] & bm)) atomicOr(&BMM[m >> 5], bm);
+                const uint32_t p = s0 + 64 * (k0 + k) + lane;
+                const uint32_t c = cv[k], m = mv[k];
+                if (p < s1 && (c | m) >= RANK_MAX_VALUE) miss = true;
+                else if (p < s1) {
+                    const uint32_t wc = BMC[c >> 5], wm = BMM[m >> 5];
+                    if ((((wc >> (c & 31)) & (wm >> (m & 31))) & 1u) == 0u) {
+                        miss = true;
+                    } else {
+                        const uint32_t rc = PRC[c >> 5] + (uint32_t)__popc(wc & ((1u << (c & 31)) - 1u));
+                        const uint32_t rm = PRM[m >> 5] + (uint32_t)__popc(wm & ((1u << (m & 31)) - 1u));
+                        const uint32_t hd = dc - 1u - rc, ld = dm - 1u - rm;
+                        LD[p] = (uint8_t)ld;
+                        ss_inc16(myrow, hd);
+                        dvp[(k0 + k) >> 1] |= hd << (16u * ((k0 + k) & 1u));
                     }
                 }
             }
         }
-        if (__ballot(big) && lane == 0) atomicOr(&NEXT[1], 1u);
-    }
-    __syncthreads();
-    // prefix popcounts: thread t owns words [8t, 8t + 8) of both bitmaps (SR_W = 8 x 1024)
-    static_assert(SR_W == 8 * 1024, "rank words per thread");
-    uint32_t bw[8], bx[8], sc = 0, sm = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        bw[j] = BMC[8 * t + j];
-        bx[j] = BMM[8 * t + j];
-        sc += (uint32_t)__popc(bw[j]);
-        sm += (uint32_t)__popc(bx[j]);
-    }
-    uint32_t dc = 0, dm = 0;
-    uint32_t pc = ss_block_excl(sc, HS, lane, w, dc);
-    __syncthreads();  // HS reused by the second scan
-    uint32_t pm = ss_block_excl(sm, HB, lane, w, dm);
-    const bool elig = NEXT[1] == 0u && dc >= 1u && dm >= 1u && dc <= SS_DIG && dm <= SS_DIG;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        PRC[8 * t + j] = (uint16_t)pc;
-        PRM[8 * t + j] = (uint16_t)pm;
-        if (elig) {  // the value of every rank, flipped to digit order (<= 256 bits in all)
-            for (uint32_t x = bw[j]; x; x &= x - 1) CV[dc - 1u - pc++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
-            for (uint32_t x = bx[j]; x; x &= x - 1) MV[dm - 1u - pm++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
-        } else {
-            pc += (uint32_t)__popc(bw[j]);
-            pm += (uint32_t)__popc(bx[j]);
-        }
-    }
-    __syncthreads();
-    if (!elig) {  // more than 256 distinct values in a dimension, or a value >= 2^18 (uniform)
-        ss_generic(a, X, WH, HS, HB, cb, C);
-        return;
-    }
-    if (t < SS_DIG) {
-        MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, MV[t]) : 0;
-        CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, CV[t]) : 0;
-    }
-    const unsigned long long ck1 = SS_CLK();
-    // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
-    const uint32_t hbits = dc > 1 ? 32u - (uint32_t)__builtin_clz(dc - 1u) : 0u;
-    const uint32_t lbits = dm > 1 ? 32u - (uint32_t)__builtin_clz(dm - 1u) : 0u;
-
-    // ---- A0: the wave's slice [s0, s1) ranked into digit pairs (kept in registers, two per
-    // dword), ld into LDS, per-wave hd counts ----
-    const uint32_t L = (C + SS_WAVES - 1) / SS_WAVES;
-    const uint32_t s0 = min(C, w * L), s1 = min(C, s0 + L);
-    uint16_t *myrow = WH + w * SS_DIG;
-    uint32_t dvp[SS_CHUNKS / 2];
-#pragma unroll
-    for (uint32_t k = 0; k < SS_CHUNKS / 2; ++k) dvp[k] = 0u;
-#pragma unroll
-    for (uint32_t k0 = 0; k0 < SS_CHUNKS; k0 += SS_LB) {
-        uint32_t cv[SS_LB], mv[SS_LB];
-#pragma unroll
-        for (uint32_t k = 0; k < SS_LB; ++k) {
-            const uint32_t p = s0 + 64 * (k0 + k) + lane;
-            cv[k] = p < s1 ? __builtin_nontemporal_load(&cpu[p]) : 0u;
-            mv[k] = p < s1 ? __builtin_nontemporal_load(&mem[p]) : 0u;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < SS_LB; ++k) {
-            const uint32_t p = s0 + 64 * (k0 + k) + lane;
-            if (p < s1) {
-                const uint32_t c = cv[k], m = mv[k];
-                const uint32_t rc = PRC[c >> 5] + (uint32_t)__popc(BMC[c >> 5] & ((1u << (c & 31)) - 1u));
-                const uint32_t rm = PRM[m >> 5] + (uint32_t)__popc(BMM[m >> 5] & ((1u << (m & 31)) - 1u));
-                const uint32_t hd = dc - 1u - rc, ld = dm - 1u - rm;
-                LD[p] = (uint8_t)ld;
-                ss_inc16(myrow, hd);
-                dvp[(k0 + k) >> 1] |= hd << (16u * ((k0 + k) & 1u));
-            }
-        }
-    }
-    __syncthreads();
+        if (__ballot(miss) && lane == 0) atomicOr(&NEXT[2], 1u);
+        __syncthreads();
+        if (NEXT[2] == 0u) return 0u;  // uniform
+        __syncthreads();               // every thread has read NEXT[2] before pass 1 clears it
+        return 1u;
+    };
+    uint32_t rr = samp ? rank_pass(0u) : 1u;
+    if (rr == 1u) rr = rank_pass(1u);
+    if (rr == 2u) return;
     ss_offsets(WH, HS, HB, t, lane, w);
     const unsigned long long ck2 = SS_CLK();
 
@@ -836,6 +863,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         if (int rs = fp_pipe_soa_take(c, SC, &soa)) return rs;
         sa.order = vals_out; sa.s_cpu = soa.s_cpu; sa.s_mem = soa.s_mem; sa.s_idx = soa.s_idx;
         sa.T = thr;
+        sa.sbm = rbm; sa.scnt = rcnt;
         const size_t lds = ss_lds_bytes(C);
         FP_HIP(hipFuncSetAttribute((const void *)k_scen_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         k_scen_sort<<<S, 1024, lds, st>>>(sa);

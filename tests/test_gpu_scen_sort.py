@@ -123,3 +123,36 @@ def test_scen_sort_single_scenario_config2(sort_path, planner, O):
     """BASELINE config 2 (one scenario, 10k x 1k) takes the per-scenario sort too."""
     cont, nodes = O.gen_scenario(0x5EED0002, 0, 10_000, 1_000, 1)
     _batch_check(planner, O, [cont], [nodes])
+
+
+@pytest.mark.parametrize("sample", ["dense", "too_many"])
+def test_scen_sort_sample_value_set(sample, planner, O):
+    """k_scen_sort ranks against the sample's value set (the first 8 scenarios) when it has at
+    most 256 values per dimension, and a workgroup that meets a value outside it (above, below or
+    between the sample's values, or >= 2^18) ranks its own scenario again (or falls back to the
+    generic sort).  A sample with too many values sends every scenario to its own values."""
+    rng = np.random.default_rng(0xA11 + len(sample))
+    S, C, N = 16, 6_000, 700
+    conts, nodes = [], []
+    for s in range(S):
+        c, n = O.gen_scenario(SEED + 91, s, C, N, 7)
+        c = [np.array(a, np.uint32) for a in c]
+        if sample == "too_many" and s == 0:
+            c[0] = rng.integers(1, 100_000, C).astype(np.uint32)
+        kind = s % 8 if s >= 8 else -1
+        j = int(rng.integers(0, C))
+        if kind == 1:
+            c[0][j] = 50 * 81 + 7          # above every sample cpu value
+        elif kind == 2:
+            c[1][j] = 1                    # below every sample mem value
+        elif kind == 3:
+            c[0][j] = 50 * 40 + 25         # between two sample cpu values
+        elif kind == 4:
+            c[1][C - 1] = 64 * 100 + 32    # the last container of the last wave's slice
+        elif kind == 5:
+            c[0][j] = (1 << 18) + 3        # past the rank tables: the generic sort
+        elif kind == 6:
+            c[1] = rng.integers(1, 100_000, C).astype(np.uint32)  # too many values: generic
+        conts.append(c)
+        nodes.append(n)
+    _batch_check(planner, O, conts, nodes, base=11)
