@@ -239,6 +239,8 @@ constexpr uint32_t SS_REG = 16;      // B: buckets of up to 64 x SS_REG containe
 constexpr size_t SS_LDS_CAP = 160 * 1024;
 constexpr uint32_t SR_W = RANK_WORDS;                  // bitmap words per dimension (values < 2^18)
 constexpr size_t SR_BYTES = (size_t)SR_W * (4 + 2) * 2;  // bitmaps u32 + prefix counts u16, both dimensions
+constexpr size_t SS_TAB_BYTES = SS_DIG * (4 + 4 + 1 + 1);  // MV, CV u32 and MB, CB u8 per digit
+constexpr size_t SS_IMG_BYTES = SR_BYTES + SS_TAB_BYTES;
 
 __host__ __device__ static inline size_t ss_align16(size_t b) { return (b + 15) & ~(size_t)15; }
 __host__ __device__ static inline size_t ss_xr_bytes(uint32_t C) {
@@ -254,13 +256,15 @@ struct ScenSortArgs {
     const uint32_t *cpu, *mem;               // [S][C] the demands
     uint32_t *order, *s_cpu, *s_mem, *s_idx; // [S][C] FFD order, sorted cpu / mem / position word
     const uint32_t *T;                       // [2 FP_BUCKETS] bucket thresholds (cpu, then mem; device)
-    const uint32_t *sbm, *scnt;              // the sample's presence bitmaps [2][RANK_WORDS] and counts (CN_*)
+    const uint32_t *scnt;                    // the sample's counts (CN_*)
+    const unsigned char *simg;               // the sample's LDS image (k_sort_image), SS_IMG_BYTES
 };
 
 // the u16 digit rows are also counted, zeroed and scanned through 32/64-bit views: these
 // types may alias the u16 entries (else type-based alias analysis may reorder them)
 typedef uint64_t __attribute__((may_alias)) ss_u64a;
 typedef uint32_t __attribute__((may_alias)) ss_u32a;
+typedef uint32_t ss_u32x4 __attribute__((ext_vector_type(4)));
 
 // lanes holding the same digit as this lane (among `valid` lanes); digits < 2^nb
 __device__ __forceinline__ uint64_t ss_match(uint32_t v, bool valid, uint32_t nb) {
@@ -463,12 +467,39 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     uint32_t dc = 0, dm = 0, hbits = 0, lbits = 0;
     uint32_t dvp[SS_CHUNKS / 2];
     unsigned long long ck1 = 0;
+    // the scenario's rows as buffer resources: range-checked loads (0 past C) without branches
+    const __amdgpu_buffer_rsrc_t rc_cpu = __builtin_amdgcn_make_buffer_rsrc((void *)cpu, (short)0, (int)(4 * C), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc_mem = __builtin_amdgcn_make_buffer_rsrc((void *)mem, (short)0, (int)(4 * C), 0x00020000);
     // one pass (inlined twice): 0 = ranked, 1 = a miss (pass 0 only), 2 = the generic sort ran
     auto rank_pass = [&](const uint32_t pass) -> uint32_t {
+        // pass 0: the sample's image in LDS layout (bitmaps + prefix counts where X will be, then
+        // the value and bucket tables: MV, CV, MB, CB are contiguous and 16-B aligned) is loaded
+        // first, then A0's first loads are issued, in flight while the image is written to LDS
+        constexpr uint32_t IMG_PT = SR_BYTES / 16 / 1024;
+        static_assert(SR_BYTES == (size_t)IMG_PT * 16 * 1024 && SS_TAB_BYTES / 16 <= 1024, "image split");
+        ss_u32x4 im[IMG_PT], imt;
+        uint32_t pcv[SS_LB], pmv[SS_LB];
+        if (pass == 0) {
+            const ss_u32x4 *src = reinterpret_cast<const ss_u32x4 *>(a.simg);
+#pragma unroll
+            for (uint32_t j = 0; j < IMG_PT; ++j) im[j] = src[t + 1024 * j];
+            imt = src[SR_BYTES / 16 + min(t, (uint32_t)(SS_TAB_BYTES / 16 - 1))];  // no branch (vmcnt)
+            __builtin_amdgcn_sched_barrier(0);  // the image's loads stay ahead of A0's (in-order vmcnt)
+#pragma unroll
+            for (uint32_t k = 0; k < SS_LB; ++k) {  // no branches: the loads stay countable (vmcnt)
+                pcv[k] = __builtin_amdgcn_raw_buffer_load_b32(rc_cpu, (int)(4 * (s0 + lane)), (int)(256 * k), 0);
+                pmv[k] = __builtin_amdgcn_raw_buffer_load_b32(rc_mem, (int)(4 * (s0 + lane)), (int)(256 * k), 0);
+            }
+        }
         for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
         if (t < 4) NEXT[t] = 0u;
         if (pass == 0) {
-            for (uint32_t i = t; i < 2 * SR_W; i += blockDim.x) BMC[i] = a.sbm[i];
+#pragma unroll
+            for (uint32_t j = 0; j < IMG_PT; ++j) reinterpret_cast<ss_u32x4 *>(ssm)[t + 1024 * j] = im[j];
+            if (t < SS_TAB_BYTES / 16) reinterpret_cast<ss_u32x4 *>(MV)[t] = imt;
+            dc = scd;
+            dm = scm;
+            __syncthreads();
         } else {
             for (uint32_t i = t; i < 2 * SR_W; i += blockDim.x) BMC[i] = 0u;
             __syncthreads();
@@ -496,42 +527,42 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
                 }
             }
             if (__ballot(big) && lane == 0) atomicOr(&NEXT[1], 1u);
-        }
-        __syncthreads();
-        // prefix popcounts: thread t owns words [8t, 8t + 8) of both bitmaps (SR_W = 8 x 1024)
-        static_assert(SR_W == 8 * 1024, "rank words per thread");
-        uint32_t bw[8], bx[8], sc = 0, sm = 0;
+            __syncthreads();
+            // prefix popcounts: thread t owns words [8t, 8t + 8) of both bitmaps (SR_W = 8 x 1024)
+            static_assert(SR_W == 8 * 1024, "rank words per thread");
+            uint32_t bw[8], bx[8], sc = 0, sm = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) {
-            bw[j] = BMC[8 * t + j];
-            bx[j] = BMM[8 * t + j];
-            sc += (uint32_t)__popc(bw[j]);
-            sm += (uint32_t)__popc(bx[j]);
-        }
-        uint32_t pc = ss_block_excl(sc, HS, lane, w, dc);
-        __syncthreads();  // HS reused by the second scan
-        uint32_t pm = ss_block_excl(sm, HB, lane, w, dm);
-        const bool elig = NEXT[1] == 0u && dc >= 1u && dm >= 1u && dc <= SS_DIG && dm <= SS_DIG;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) {
-            PRC[8 * t + j] = (uint16_t)pc;
-            PRM[8 * t + j] = (uint16_t)pm;
-            if (elig) {  // the value of every rank, flipped to digit order (<= 256 bits in all)
-                for (uint32_t x = bw[j]; x; x &= x - 1) CV[dc - 1u - pc++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
-                for (uint32_t x = bx[j]; x; x &= x - 1) MV[dm - 1u - pm++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
-            } else {
-                pc += (uint32_t)__popc(bw[j]);
-                pm += (uint32_t)__popc(bx[j]);
+            for (uint32_t j = 0; j < 8; ++j) {
+                bw[j] = BMC[8 * t + j];
+                bx[j] = BMM[8 * t + j];
+                sc += (uint32_t)__popc(bw[j]);
+                sm += (uint32_t)__popc(bx[j]);
             }
-        }
-        __syncthreads();
-        if (!elig) {  // more than 256 distinct values in a dimension, or a value >= 2^18 (uniform)
-            ss_generic(a, X, WH, HS, HB, cb, C);
-            return 2u;
-        }
-        if (t < SS_DIG) {
-            MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, MV[t]) : 0;
-            CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, CV[t]) : 0;
+            uint32_t pc = ss_block_excl(sc, HS, lane, w, dc);
+            __syncthreads();  // HS reused by the second scan
+            uint32_t pm = ss_block_excl(sm, HB, lane, w, dm);
+            const bool elig = NEXT[1] == 0u && dc >= 1u && dm >= 1u && dc <= SS_DIG && dm <= SS_DIG;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                PRC[8 * t + j] = (uint16_t)pc;
+                PRM[8 * t + j] = (uint16_t)pm;
+                if (elig) {  // the value of every rank, flipped to digit order (<= 256 bits in all)
+                    for (uint32_t x = bw[j]; x; x &= x - 1) CV[dc - 1u - pc++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
+                    for (uint32_t x = bx[j]; x; x &= x - 1) MV[dm - 1u - pm++] = (8 * t + j) * 32 + (uint32_t)__builtin_ctz(x);
+                } else {
+                    pc += (uint32_t)__popc(bw[j]);
+                    pm += (uint32_t)__popc(bx[j]);
+                }
+            }
+            __syncthreads();
+            if (!elig) {  // more than 256 distinct values in a dimension, or a value >= 2^18 (uniform)
+                ss_generic(a, X, WH, HS, HB, cb, C);
+                return 2u;
+            }
+            if (t < SS_DIG) {
+                MB[t] = a.kpack && t < dm ? (uint8_t)ss_bucket(a.T + FP_BUCKETS, MV[t]) : 0;
+                CB[t] = a.kpack && t < dc ? (uint8_t)ss_bucket(a.T, CV[t]) : 0;
+            }
         }
         ck1 = SS_CLK();
         // bits of the largest digit (dc - 1, dm - 1): the match masks test only those
@@ -549,8 +580,13 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
 #pragma unroll
             for (uint32_t k = 0; k < SS_LB; ++k) {
                 const uint32_t p = s0 + 64 * (k0 + k) + lane;
-                cv[k] = p < s1 ? __builtin_nontemporal_load(&cpu[p]) : 0u;
-                mv[k] = p < s1 ? __builtin_nontemporal_load(&mem[p]) : 0u;
+                if (pass == 0 && k0 == 0) {
+                    cv[k] = pcv[k];
+                    mv[k] = pmv[k];
+                } else {
+                    cv[k] = p < s1 ? __builtin_nontemporal_load(&cpu[p]) : 0u;
+                    mv[k] = p < s1 ? __builtin_nontemporal_load(&mem[p]) : 0u;
+                }
             }
 #pragma unroll
             for (uint32_t k = 0; k < SS_LB; ++k) {
@@ -732,6 +768,33 @@ __global__ void k_thresholds(uint32_t *__restrict__ cnt, const uint32_t *__restr
     for (int k = 0; k < FP_BUCKETS; ++k) thr[d * FP_BUCKETS + k] = T[k];
 }
 
+// The sample's ranks as k_scen_sort's LDS image (pass 0 copies it): presence bitmaps [2][SR_W] u32,
+// exclusive prefix counts [2][SR_W] u16, then per digit the mem and cpu values (digit d = rank
+// dc-1-d) and their bucket ids.  Written only when the sample has <= 256 values per dimension, all
+// below 2^18 (k_scen_sort tests the same counts).
+__global__ __launch_bounds__(1024) void k_sort_image(const uint32_t *__restrict__ bm, const uint32_t *__restrict__ pre,
+                                                     const uint32_t *__restrict__ val, const uint32_t *__restrict__ cnt,
+                                                     const uint32_t *__restrict__ T, uint32_t kpack,
+                                                     unsigned char *__restrict__ img) {
+    const uint32_t dc = cnt[CN_DC], dm = cnt[CN_DM], t = threadIdx.x;
+    if (cnt[CN_OVER] != 0u || dc - 1u >= SS_DIG || dm - 1u >= SS_DIG) return;
+    uint32_t *ibm = reinterpret_cast<uint32_t *>(img);
+    uint16_t *ipr = reinterpret_cast<uint16_t *>(ibm + 2 * SR_W);
+    for (uint32_t i = t; i < 2 * SR_W; i += blockDim.x) {
+        ibm[i] = bm[i];
+        ipr[i] = (uint16_t)pre[i];
+    }
+    uint32_t *mv = reinterpret_cast<uint32_t *>(img + SR_BYTES), *cv = mv + SS_DIG;
+    uint8_t *mb = reinterpret_cast<uint8_t *>(cv + SS_DIG), *cbk = mb + SS_DIG;
+    if (t < SS_DIG) {
+        const uint32_t c = t < dc ? val[dc - 1u - t] : 0u, m = t < dm ? val[RANK_MAX_VALUE + dm - 1u - t] : 0u;
+        cv[t] = c;
+        mv[t] = m;
+        cbk[t] = kpack && t < dc ? (uint8_t)ss_bucket(T, c) : 0;
+        mb[t] = kpack && t < dm ? (uint8_t)ss_bucket(T + FP_BUCKETS, m) : 0;
+    }
+}
+
 }  // namespace
 
 #ifdef FP_PIPE_STATS
@@ -772,7 +835,8 @@ static int place_ws_need(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, size_t *
     sort_tmp = t > sort_tmp ? t : sort_tmp;
     const size_t pipe_ws = fp_pipe_ws_bytes(c, S, C, N);
     if (pipe_ws == 0) return FP_EOVERFLOW;
-    const size_t rank_ws = 2 * (2 * RANK_WORDS * 4 + RANK_MAX_VALUE * 4) + CN_WORDS * 4 + 2 * FP_BUCKETS * 4 + 3 * 256;
+    const size_t rank_ws = 2 * (2 * RANK_WORDS * 4 + RANK_MAX_VALUE * 4) + CN_WORDS * 4 + 2 * FP_BUCKETS * 4 + 3 * 256
+                           + SS_IMG_BYTES + 256;
     *need = SC * (8 * 2 + 4 * 2) + (S + 1) * 4 + sort_tmp + pipe_ws + rank_ws + 16 * 256;
     *sort_tmp_out = sort_tmp;
     return FP_OK;
@@ -827,7 +891,9 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     uint32_t *rval = (uint32_t *)fp_ws_take(c, 2 * RANK_MAX_VALUE * 4);
     uint32_t *rcnt = (uint32_t *)fp_ws_take(c, CN_WORDS * 4);
     uint32_t *thr = (uint32_t *)fp_ws_take(c, 2 * FP_BUCKETS * 4);
-    if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !rbm || !rpre || !rval || !rcnt || !thr)
+    unsigned char *simg = (unsigned char *)fp_ws_take(c, SS_IMG_BYTES);
+    if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !rbm || !rpre || !rval || !rcnt || !thr ||
+        !simg)
         return FP_ENOMEM;
 
     // ---- 1-2: the bucket thresholds (device), from the distinct values and bounds of a sample:
@@ -863,7 +929,10 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         if (int rs = fp_pipe_soa_take(c, SC, &soa)) return rs;
         sa.order = vals_out; sa.s_cpu = soa.s_cpu; sa.s_mem = soa.s_mem; sa.s_idx = soa.s_idx;
         sa.T = thr;
-        sa.sbm = rbm; sa.scnt = rcnt;
+        sa.scnt = rcnt;
+        sa.simg = simg;
+        k_sort_image<<<1, 1024, 0, st>>>(rbm, rpre, rval, rcnt, thr, sa.kpack, simg);
+        FP_HIP(hipGetLastError());
         const size_t lds = ss_lds_bytes(C);
         FP_HIP(hipFuncSetAttribute((const void *)k_scen_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         k_scen_sort<<<S, 1024, lds, st>>>(sa);
