@@ -470,20 +470,35 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     // the scenario's rows as buffer resources: range-checked loads (0 past C) without branches
     const __amdgpu_buffer_rsrc_t rc_cpu = __builtin_amdgcn_make_buffer_rsrc((void *)cpu, (short)0, (int)(4 * C), 0x00020000);
     const __amdgpu_buffer_rsrc_t rc_mem = __builtin_amdgcn_make_buffer_rsrc((void *)mem, (short)0, (int)(4 * C), 0x00020000);
+    // the sample's image: 16-B units of BMC, BMM, PRC, PRM up to the largest sample value's word,
+    // then the tables; unit u -> image byte offset (returned) and LDS byte offset (dst)
+    const uint32_t smc = a.scnt[2], smm = a.scnt[3];  // the sample's largest values (k_rank_tables)
+    const uint32_t iwc = (smc >> 5) + 1u, iwm = (smm >> 5) + 1u;
+    const uint32_t ib1 = (4u * iwc + 15u) / 16u, ib2 = ib1 + (4u * iwm + 15u) / 16u;
+    const uint32_t ib3 = ib2 + (2u * iwc + 15u) / 16u, ib4 = ib3 + (2u * iwm + 15u) / 16u;
+    const uint32_t img_units = ib4 + (uint32_t)(SS_TAB_BYTES / 16);
+    const uint32_t tab_dst = (uint32_t)(reinterpret_cast<unsigned char *>(MV) - ssm);
+    auto img_unit = [&](uint32_t u, uint32_t &dst) -> uint32_t {
+        const uint32_t src = u < ib1   ? 16u * u
+                             : u < ib2 ? 4u * SR_W + 16u * (u - ib1)
+                             : u < ib3 ? 8u * SR_W + 16u * (u - ib2)
+                             : u < ib4 ? 10u * SR_W + 16u * (u - ib3)
+                                       : (uint32_t)SR_BYTES + 16u * (u - ib4);
+        dst = u < ib4 ? src : tab_dst + 16u * (u - ib4);
+        return src;
+    };
     // one pass (inlined twice): 0 = ranked, 1 = a miss (pass 0 only), 2 = the generic sort ran
     auto rank_pass = [&](const uint32_t pass) -> uint32_t {
-        // pass 0: the sample's image in LDS layout (bitmaps + prefix counts where X will be, then
-        // the value and bucket tables: MV, CV, MB, CB are contiguous and 16-B aligned) is loaded
-        // first, then A0's first loads are issued, in flight while the image is written to LDS
-        constexpr uint32_t IMG_PT = SR_BYTES / 16 / 1024;
-        static_assert(SR_BYTES == (size_t)IMG_PT * 16 * 1024 && SS_TAB_BYTES / 16 <= 1024, "image split");
-        ss_u32x4 im[IMG_PT], imt;
+        // pass 0: the part of the sample's image the sample's values use (bitmap and prefix words
+        // up to the largest value, in LDS layout where X will be; then the value and bucket
+        // tables: MV, CV, MB, CB are contiguous and 16-B aligned) is loaded first, one 16-B unit
+        // per thread, then A0's first loads are issued, in flight while the image is written
+        ss_u32x4 imv;
+        uint32_t isrc = 0, idst = 0;
         uint32_t pcv[SS_LB], pmv[SS_LB];
         if (pass == 0) {
-            const ss_u32x4 *src = reinterpret_cast<const ss_u32x4 *>(a.simg);
-#pragma unroll
-            for (uint32_t j = 0; j < IMG_PT; ++j) im[j] = src[t + 1024 * j];
-            imt = src[SR_BYTES / 16 + min(t, (uint32_t)(SS_TAB_BYTES / 16 - 1))];  // no branch (vmcnt)
+            isrc = img_unit(min(t, img_units - 1u), idst);
+            imv = *reinterpret_cast<const ss_u32x4 *>(a.simg + isrc);  // no branch (vmcnt)
             __builtin_amdgcn_sched_barrier(0);  // the image's loads stay ahead of A0's (in-order vmcnt)
 #pragma unroll
             for (uint32_t k = 0; k < SS_LB; ++k) {  // no branches: the loads stay countable (vmcnt)
@@ -494,9 +509,11 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
         for (uint32_t i = t; i < SS_WAVES * SS_DIG / 2; i += blockDim.x) reinterpret_cast<ss_u32a *>(WH)[i] = 0u;
         if (t < 4) NEXT[t] = 0u;
         if (pass == 0) {
-#pragma unroll
-            for (uint32_t j = 0; j < IMG_PT; ++j) reinterpret_cast<ss_u32x4 *>(ssm)[t + 1024 * j] = im[j];
-            if (t < SS_TAB_BYTES / 16) reinterpret_cast<ss_u32x4 *>(MV)[t] = imt;
+            if (t < img_units) *reinterpret_cast<ss_u32x4 *>(ssm + idst) = imv;
+            for (uint32_t u = t + 1024; u < img_units; u += 1024) {  // sample values above ~2^16
+                const uint32_t so = img_unit(u, idst);
+                *reinterpret_cast<ss_u32x4 *>(ssm + idst) = *reinterpret_cast<const ss_u32x4 *>(a.simg + so);
+            }
             dc = scd;
             dm = scm;
             __syncthreads();
@@ -592,7 +609,8 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
             for (uint32_t k = 0; k < SS_LB; ++k) {
                 const uint32_t p = s0 + 64 * (k0 + k) + lane;
                 const uint32_t c = cv[k], m = mv[k];
-                if (p < s1 && (c | m) >= RANK_MAX_VALUE) miss = true;
+                // pass 0 copied the words up to the sample's largest values (all below 2^18)
+                if (p < s1 && (pass == 0 ? c > smc || m > smm : (c | m) >= RANK_MAX_VALUE)) miss = true;
                 else if (p < s1) {
                     const uint32_t wc = BMC[c >> 5], wm = BMM[m >> 5];
                     if ((((wc >> (c & 31)) & (wm >> (m & 31))) & 1u) == 0u) {
