@@ -9,10 +9,11 @@
 //      raw bounds (max, smallest positive) in the same pass
 //   2. k_thresholds: the pipeline's bucket thresholds (spread over the distinct values, or
 //      geometric between the bounds), into device memory
-//   3a. scenarios of at most ~50k containers (host-known): the per-scenario LDS sort below
-//      (k_scen_sort: the scenario's own dense ranks), which falls back, in the same workgroup, to a
-//      generic stable LSD sort of the raw values when the scenario has more than 256 distinct
-//      values or values >= 2^18
+//   3a. scenarios of at most ~50k containers (host-known): k_sort_image (the sample's ranks in
+//      LDS layout), then the per-scenario LDS sort below (k_scen_sort: digits are ranks in the
+//      sample's value set, or in the scenario's own when it holds a value the sample lacks), which
+//      falls back, in the same workgroup, to a generic stable LSD sort of the raw values when the
+//      scenario has more than 256 distinct values or values >= 2^18
 //   3b. larger scenarios: k_make_keys (full-width key (~cpu << 32 | ~mem), value = index) and a
 //      stable rocprim radix sort over 64 bits, segmented per scenario when there are several
 //   4. k_ffd_pipe   : (fp_pipe.hip) per scenario, containers in key order stream
@@ -211,13 +212,15 @@ __global__ void k_argmin_cost(const uint64_t *__restrict__ cost, uint32_t n, uin
 //
 // Every scenario is sorted into FFD order (cpu desc, mem desc, index asc) by one workgroup
 // of 1024 threads in LDS.  It writes the order and the sorted cpu / mem / position words
-// itself, so no radix keys, onesweep passes or key decode touch HBM.  The digits are the
-// scenario's own dense value ranks, flipped so that an ascending digit means a descending demand:
-// hd = dc-1-rank(cpu), ld = dm-1-rank(mem), each below 256.  k_scen_sort, one workgroup per
-// scenario:
-//   R   presence bitmaps of the scenario's cpu and mem values (v < 2^18) in LDS, their prefix
-//       popcounts and the value of every rank: dc, dm and the eligibility of the digit sort
-//       (<= 256 values per dimension) are the scenario's own, decided in the workgroup
+// itself, so no radix keys, onesweep passes or key decode touch HBM.  The digits are value ranks
+// in a set that holds every value of the scenario, flipped so that an ascending digit means a
+// descending demand: hd = dc-1-rank(cpu), ld = dm-1-rank(mem), each below 256.  k_scen_sort, one
+// workgroup per scenario:
+//   R   presence bitmaps of the value set (v < 2^18) in LDS, their prefix popcounts and the value
+//       of every rank.  Pass 0 copies the sample's (k_sort_image); a value of the scenario outside
+//       it (found in A0) sends the workgroup to pass 1, the scenario's own values from one
+//       streaming pass: dc, dm and the eligibility of the digit sort (<= 256 values per
+//       dimension) are then the scenario's own, decided in the workgroup
 //   A0  each wave loads its contiguous slice of the scenario, ranks it into digit pairs (kept in
 //       registers), keeps ld[j] in LDS and counts the hd digits (packed u16 LDS atomics); one
 //       scan gives every (wave, digit) its offset
