@@ -39,6 +39,27 @@ __global__ __launch_bounds__(kBlock) void k_part_count(const uint8_t *__restrict
     }
 }
 
+// The whole partition in one launch for n <= 1024 (a stage of a fleet.kdl: config 1), one thread
+// per vertex: the three kernels below cost a launch each.
+__global__ __launch_bounds__(1024) void k_part_small(const uint8_t *__restrict__ hd, uint32_t n,
+                                                     uint32_t *__restrict__ perm) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t i = threadIdx.x, lane = i & 63, w = i >> 6;
+    const bool z = i < n && hd[i] == 0;
+    const uint64_t m = __ballot(z);
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (uint32_t q = 0; q < 16; ++q) {
+        woff += q < w ? wsum[q] : 0u;
+        tot += wsum[q];
+    }
+    if (i < n) {
+        const uint32_t zb = woff + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));  // zeros before i
+        perm[z ? zb : tot + i - zb] = i;
+    }
+}
+
 // Exclusive scan of block counts by one block; writes total to blk_off[nb].
 __global__ __launch_bounds__(1024) void k_part_scan(const uint32_t *__restrict__ blk_zero,
                                                     uint32_t nb, uint32_t *__restrict__ blk_off) {
@@ -888,6 +909,14 @@ int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
     if (V == 0) return FP_OK;
     if (!g->has_deps || !perm) return FP_EINVAL;
     hipStream_t st = c->stream;
+    if (V <= 1024 && fp_opt(c, FP_OPT_LEVEL_SMALL, 1) != 0) {  // one launch (FP_OPT_LEVEL_SMALL = 0: three)
+        hipEvent_t ev;
+        fp_prof_begin(c, FP_K_LEVEL, &ev);
+        k_part_small<<<1, 1024, 0, st>>>(g->has_deps, V, perm);
+        FP_HIP(hipGetLastError());
+        fp_prof_end(c, FP_K_LEVEL, ev);
+        return FP_OK;
+    }
     const uint32_t nb = (uint32_t)((V + kSpan - 1) / kSpan);
     int rc = fp_ws_reserve(c, (size_t)(nb + 1) * 8 + 1024);
     if (rc) return rc;

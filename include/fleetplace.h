@@ -162,7 +162,7 @@ enum fp_option {
     FP_OPT_SYSTOLIC_VALU = 16,/* 1 = VALU-only systolic steps (fp_pipe_sysv.h), 0 = exec-masked  */
     FP_OPT_LINK_PUBLISH = 17, /* full slots per head publish on unbounded global links (auto 32) */
     FP_OPT_LEVEL_SORT = 18,   /* levelizer start order: 0 = radix sort, auto = LSD counting sort   */
-    FP_OPT_LEVEL_SMALL = 19,  /* 0 = no one-launch levelizer for graphs of <= 512 vertices           */
+    FP_OPT_LEVEL_SMALL = 19,  /* 0 = no one-launch levelizer (<= 512 vertices) / legacy order (<= 1024) */
     FP_OPT_COUNT = 20
 };
 int fp_ctx_set_option(fp_ctx *ctx, int option, int64_t value);

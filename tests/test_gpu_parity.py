@@ -22,8 +22,12 @@ def test_order_by_dependencies_reference_kats(kats, planner):
         assert order_by_dependencies(case["services"], _flow(case), planner) == case["expected"], case["source"]
 
 
+@pytest.mark.parametrize("small", [1, 0])
 @pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1023, 1024, 1025, 100_000, 1_000_000])
-def test_legacy_order_random(n, planner, O):
+def test_legacy_order_random(n, small, planner, O, opts):
+    """Up to 1024 vertices the partition is one launch (k_part_small); FP_OPT_LEVEL_SMALL = 0 keeps
+    the three-kernel path there too."""
+    opts(level_small=small)
     rng = np.random.default_rng(n)
     hd = (rng.random(n) < 0.37).astype(np.uint8)
     if n == 0:
