@@ -215,13 +215,17 @@ def cpu_single_thread_legs(gpu):
     out = {}
     rp, col, hd = gpu["config5"]["graph"]
     O.legacy_order(hd)
-    a1_ms, _ = _median_ms(lambda: O.legacy_order(hd), 5)
+    a1_ms, a1_perm = _median_ms(lambda: O.legacy_order(hd), 5)
+    g_a1 = gpu["config5"]["legacy"]
     O.levelize(rp, col, hd)
     lv_ms, (el, eo, en) = _median_ms(lambda: O.levelize(rp, col, hd), 5)
     gl, go, gn = gpu["config5"]["levels"]
     lv_ok = bool(np.array_equal(gl, el) and np.array_equal(go, eo) and gn == en)
     V, E = hd.size, col.size
-    out["legacy_order_config5"] = {"ms": a1_ms, "unit_value": V / (a1_ms / 1e3), "unit": "vertices/s", "cores": 1}
+    out["legacy_order_config5"] = {"ms": a1_ms, "unit_value": V / (a1_ms / 1e3), "unit": "vertices/s", "cores": 1,
+                                   "gpu_ms_per_step": g_a1["ms_per_step"], "gpu_kernel_ms": g_a1["kernel_ms"],
+                                   "gpu_unit_value": g_a1["unit_value"],
+                                   "gpu_bit_exact": bool(np.array_equal(g_a1["perm"], a1_perm))}
     out["levelize_config5"] = {"ms": lv_ms, "unit_value": (V + E) / (lv_ms / 1e3), "unit": "(V+E)/s", "cores": 1,
                                "gpu_bit_exact": lv_ok}
     cont2, nodes2 = O.gen_scenario(SEED2, 0, C2, N2, FLAGS2)
@@ -291,8 +295,9 @@ def config1_leg(planner, reps=200):
     cargo = shutil.which("cargo")
     out["rust"] = ("cargo found at " + cargo + "; the Rust crate is not built by the bench") if cargo else \
         "Rust not available; C restatement used (oracle/fp_oracle.c, engine.rs:67-85 restated)"
-    out["note"] = ("GPU = KDL front end + stage graph on the host + fp_legacy_order + fp_levelize (+ the host-pointer "
-                   "staging) per plan; CPU = stage graph + fpo_legacy_order + fpo_levelize, single thread")
+    out["note"] = ("GPU = KDL front end + stage graph on the host + ONE fp_plan_stage call (k_plan_small: A1 order, "
+                   "A2 levels and start order in one kernel, inputs and results in mapped pinned host memory); "
+                   "CPU = stage graph + fpo_legacy_order + fpo_levelize, single thread")
     return out
 
 
@@ -448,6 +453,19 @@ def levelize_leg(planner, dev, steps):
     k_ms, k_n = planner.kernel_stats(FP_K_LEVEL)
     planner.profile(False)
     step_s, kernel_s = el / steps, k_ms / max(k_n, 1) / 1e3
+    # A1 (engine.rs:67-85) on the same 1M vertices: fp_dev_legacy_order, timed beside the C
+    # restatement's cpu_single_thread.legacy_order_config5 (checked against it there)
+    perm_t = torch.empty(V, dtype=torch.int32, device=dev)
+    planner.dev_legacy_order(hd_t, perm_t)
+    planner.sync()
+    planner.profile(True)
+    a1_el = timed(steps, lambda: planner.dev_legacy_order(hd_t, perm_t), lambda: torch.cuda.synchronize(dev),
+                  lambda: None)
+    planner.sync()
+    a1_k_ms, a1_k_n = planner.kernel_stats(FP_K_LEVEL)
+    planner.profile(False)
+    legacy = {"ms_per_step": a1_el / steps * 1e3, "kernel_ms": a1_k_ms / max(a1_k_n, 1), "unit_value": V / (a1_el / steps),
+              "unit": "vertices/s", "perm": perm_t.cpu().numpy().view(np.uint32)}
     nbytes = 16 * V + 12 * E + 4
     levels = level_t.cpu().numpy().view(np.uint32)
     out = {"workload": "BASELINE config 5a: levelize the 1M-vertex depends_on DAG (deep chains + wide fan-out, "
@@ -459,7 +477,7 @@ def levelize_leg(planner, dev, steps):
                         "frac": nbytes / kernel_s / 1e9 / HBM_PEAK_GBPS, "traffic": None,
                         "algorithmic_bytes": nbytes,
                         "limiter": "latency of the longest dependency chain (500 levels of chains)"}}
-    return out, (rp, col, hd), level_t, (levels, order_t.cpu().numpy().view(np.uint32), int(ncyc_t.item()))
+    return out, (rp, col, hd), level_t, (levels, order_t.cpu().numpy().view(np.uint32), int(ncyc_t.item())), legacy
 
 
 # VALU lane-operations per container x node evaluation in k_feas's inner loop (no bitmap):
@@ -623,10 +641,10 @@ def worker(args):
             gpu["config3"] = {"plan": plan}
             out["config3"] = dict({"workload": "BASELINE config 3: 1 scenario x 1M containers x 100k nodes, "
                                                "ports+anti-affinity+labels"}, **r)
-            lv, graph, level_t, levels = levelize_leg(planner, dev, 5)
+            lv, graph, level_t, levels, legacy = levelize_leg(planner, dev, 5)
             r, plan = single_leg(planner, dev, "config5", SEED5, graph[2].size, N5, FLAGS, args.config3_steps, 1,
                                  level_t=level_t)
-            gpu["config5"] = {"plan": plan, "graph": graph, "levels": levels}
+            gpu["config5"] = {"plan": plan, "graph": graph, "levels": levels, "legacy": legacy}
             out["config5"] = {"workload": "BASELINE config 5: levelize the 1M-vertex DAG, then place its 1M "
                                           "containers on 100k nodes (CYCLE members skipped)",
                               "levelize": lv, "place": r,

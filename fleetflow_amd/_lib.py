@@ -19,6 +19,7 @@ FP_NONE = 0xFFFFFFFF
 REASON_OK, REASON_NOFIT, REASON_CYCLE = 0, 1, 2
 FP_K_PLACE, FP_K_SORT, FP_K_FEAS, FP_K_LEVEL, FP_K_GEN = 0, 1, 2, 3, 4
 # context options (fleetplace.h enum fp_option); FP_OPT_AUTO = the production default
+# ("segsort" is ignored by the library and kept for ABI stability)
 FP_OPT_AUTO = -1
 OPTIONS = {"pipe_w": 0, "pipe_seg": 1, "pipe_r": 2, "pipe_lag": 3, "link_slots": 4, "link_bounded": 5,
            "pipe_flush": 6, "spin_ticks": 7, "kpack": 8, "scen_sort": 9, "segsort": 10, "systolic": 11,
@@ -82,6 +83,8 @@ SIGNATURES = {
     "fp_place": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p, u8p]),
     "fp_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),
     "fp_feasibility": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p, u64p]),
+    "fp_plan_stage": (ct.c_int, [vp, ct.POINTER(FpGraph), ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p,
+                                 u32p, u32p, u32p, u32p, u32p, u8p]),
     "fp_dev_legacy_order": (ct.c_int, [vp, ct.POINTER(FpGraph), vp]),
     "fp_dev_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), vp, vp, vp]),
     "fp_dev_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),

@@ -73,6 +73,7 @@ extern "C" void fp_ctx_destroy(fp_ctx *c) {
     if (c->h_in_ev) (void)hipEventSynchronize(c->h_in_ev);
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_in_ev) (void)hipEventDestroy(c->h_in_ev);
+    if (c->h_map) (void)hipHostFree(c->h_map);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -396,8 +397,9 @@ static int copy_back_span(fp_ctx *c, const OutCopy *o, int n) {
 
 extern "C" int fp_legacy_order(fp_ctx *c, const fp_graph *g, uint32_t *perm_out) {
     if (!c || !g || (g->n_vertices && (!g->has_deps || !perm_out))) return FP_EINVAL;
-    fp_host_err_scope es(c);
     FP_HIP(hipSetDevice(c->device));
+    fp_host_err_scope es(c);
+    if (es.rc) return es.rc;
     const size_t V = g->n_vertices;
     int rc = fp_stage_reserve(c, 2 * V * 4 + 8192);
     if (rc) return rc;
@@ -431,6 +433,7 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
     // the CSR is validated on the device (k_check_csr, k_indeg): FP_ECORRUPT
     FP_HIP(hipSetDevice(c->device));
     fp_host_err_scope es(c);
+    if (es.rc) return es.rc;
     int rc = fp_stage_reserve(c, (V + 1) * 4 + E * 4 + V + 2 * V * 4 + 16 * 256);
     if (rc) return rc;
     fp_stage_reset(c);
@@ -453,7 +456,6 @@ extern "C" int fp_levelize(fp_ctx *c, const fp_graph *g, uint32_t *level_out, ui
 }
 
 static int batch_host(fp_ctx *c, const fp_batch *b) {
-    fp_host_err_scope es(c);
     const size_t S = b->n_scen, C = b->n_containers, N = b->n_nodes;
     const size_t SC = S * C, SN = S * N;
     if (S && C && (!b->cpu_m || !b->mem_mib || !b->req_labels || !b->conflict || !b->assign ||
@@ -463,6 +465,8 @@ static int batch_host(fp_ctx *c, const fp_batch *b) {
                    !b->schedulable))
         return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
+    fp_host_err_scope es(c);
+    if (es.rc) return es.rc;
     int rc = fp_stage_reserve(c, SC * (4 * 6 + 1) + SN * (4 * 4 + 1) + S * 8 + 16 * 256);
     if (rc) return rc;
     fp_stage_reset(c);
@@ -531,6 +535,7 @@ extern "C" int fp_feasibility(fp_ctx *c, const fp_containers *cs, const fp_nodes
         return FP_EINVAL;
     FP_HIP(hipSetDevice(c->device));
     fp_host_err_scope es(c);
+    if (es.rc) return es.rc;
     int rc = fp_stage_reserve(c, C * 24 + N * 17 + (bitmap_out ? WC * N * 8 : 0) + 16 * 256);
     if (rc) return rc;
     fp_stage_reset(c);

@@ -50,6 +50,11 @@ struct fp_ctx {
     char *h_in = nullptr;
     size_t h_in_cap = 0;
     hipEvent_t h_in_ev = nullptr;
+    // mapped pinned host memory of fp_plan_stage's one-launch path (fp_small.hip): the kernel reads
+    // its inputs from and writes its results to it (h_map on the host, d_map on the device)
+    char *h_map = nullptr;
+    void *d_map = nullptr;
+    size_t h_map_cap = 0;
     // profiling
     bool profile = false;
     struct Rec { int kid; hipEvent_t a, b; };
@@ -85,11 +90,15 @@ static inline int64_t fp_opt(const fp_ctx *c, int k, int64_t dflt) {
 // a host-pointer call's own kernel error word for its duration (fp_internal.h fp_ctx)
 // The word is cleared on entry (stream-ordered), so an error a previous host call's kernels
 // raised after that call exited early (a HIP failure, ENOMEM mid-call) is not reported here.
+// Built after hipSetDevice(c->device) (the clear is issued on the context's device); `rc` is the
+// clear's result, which the caller returns when it failed.
 struct fp_host_err_scope {
     fp_ctx *c;
+    int rc;
     explicit fp_host_err_scope(fp_ctx *cc) : c(cc) {
         c->d_err = c->d_err_base + fp_ctx::HOST_ERR;
-        (void)hipMemsetAsync(c->d_err, 0, 4, c->stream);
+        const hipError_t e = hipMemsetAsync(c->d_err, 0, 4, c->stream);
+        rc = e == hipSuccess ? FP_OK : fp_hip_fail(e);
     }
     ~fp_host_err_scope() { c->d_err = c->d_err_base; }
 };

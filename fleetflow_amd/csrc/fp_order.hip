@@ -9,6 +9,7 @@
 //    launch per level).  level(v) = max(has_deps(v), max_{d->v} level(d)+1) is unique,
 //    so neither schedule (nor the atomic order inside it) can change the result.
 #include "fp_internal.h"
+#include "fp_small.h"
 #include <rocprim/device/device_radix_sort.hpp>
 #include <stdlib.h>
 #include <string.h>
@@ -790,11 +791,12 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
 // ---- small graphs: the whole levelization in one workgroup ---------------------------------
 // A graph of at most LS_V vertices and LS_E edges (a fleet.kdl stage: config 1) is levelized by
 // ONE launch: CSR check, in-degrees, level-synchronous Kahn and the stable (level, index) start
-// order, all in LDS.  The general path's ~25 launches and memsets cost ~100 us of submission for
-// a 3-service stage; this one costs one.  (A round per level costs two workgroup barriers, so
-// LS_V bounds the depth too.)  FP_OPT_LEVEL_SMALL = 0 keeps the general path.
-constexpr uint32_t LS_V = 512, LS_E = 8192;
-__host__ __device__ inline size_t ls_lds_bytes(uint32_t V) { return ((size_t)V * 4 + 16 + 2) * 4; }
+// order, all in LDS (fps::ls_levels, fp_small.h).  The general path's ~25 launches and memsets
+// cost ~100 us of submission for a 3-service stage; this one costs one.  FP_OPT_LEVEL_SMALL = 0
+// keeps the general path.
+using fps::LS_E;
+using fps::LS_V;
+__host__ __device__ inline size_t ls_lds_bytes(uint32_t V) { return fps::ls_words(V) * 4; }
 
 __global__ __launch_bounds__(1024) void k_lvl_small(const uint32_t *__restrict__ row_ptr,
                                                     const uint32_t *__restrict__ col,
@@ -802,99 +804,12 @@ __global__ __launch_bounds__(1024) void k_lvl_small(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ level, uint32_t *__restrict__ order,
                                                     uint32_t *__restrict__ ncyc_out, uint32_t *__restrict__ err) {
     extern __shared__ uint32_t lsm[];
-    // ctl: [0] bad [1] count fr0 [2] count fr1 [3] max level [4] cycle vertices; then deg, lvl and the
-    // two frontiers, fr1 with 2 spare words: the key starts reuse fr0 + fr1 (ck + 1 <= V + 2 bins)
-    uint32_t *ctl = lsm, *deg = lsm + 16, *lvl = deg + V, *fr0 = lvl + V, *fr1 = fr0 + V;
-    const uint32_t t = threadIdx.x, lane = t & 63;
-    if (t < 16) ctl[t] = 0u;
-    for (uint32_t v = t; v < V; v += blockDim.x) deg[v] = 0u;
-    __syncthreads();
-    // CSR check (the general path's k_check_csr / k_indeg conditions) and in-degrees
-    bool bad = false;
-    for (uint32_t v = t; v < V; v += blockDim.x) bad |= row_ptr[v + 1] < row_ptr[v];
-    if (t == 0) bad |= row_ptr[0] != 0u || row_ptr[V] != E;
-    for (uint32_t e = t; e < E; e += blockDim.x) {
-        const uint32_t w = col[e];
-        if (w >= V) bad = true;
-        else atomicAdd(&deg[w], 1u);
+    const uint32_t nc = fps::ls_levels(row_ptr, col, hd, V, E, lsm, level, order);
+    if (nc == FP_NONE) {
+        if (threadIdx.x == 0) atomicMax(err, (uint32_t)(-FP_ECORRUPT));
+        return;
     }
-    if (bad) atomicOr(&ctl[0], 1u);
-    __syncthreads();
-    if (ctl[0]) {
-        if (t == 0) atomicMax(err, (uint32_t)(-FP_ECORRUPT));
-        return;  // uniform
-    }
-    for (uint32_t v = t; v < V; v += blockDim.x) {
-        lvl[v] = hd[v] ? 1u : 0u;
-        if (deg[v] == 0u) fr0[atomicAdd(&ctl[1], 1u)] = v;
-    }
-    __syncthreads();
-    // level-synchronous Kahn: the frontier in LDS, one round per level
-    uint32_t *cur = fr0, *nxt = fr1;
-    uint32_t ci = 1;
-    while (true) {
-        const uint32_t n = ctl[ci];
-        if (n == 0u) break;  // uniform (read after the barrier)
-        for (uint32_t i = t; i < n; i += blockDim.x) {
-            const uint32_t u = cur[i], lu1 = lvl[u] + 1u;
-            atomicMax(&ctl[3], lvl[u]);
-            for (uint32_t e = row_ptr[u], e1 = row_ptr[u + 1]; e < e1; ++e) {
-                const uint32_t w = col[e];
-                atomicMax(&lvl[w], lu1);
-                if (atomicSub(&deg[w], 1u) == 1u) nxt[atomicAdd(&ctl[3 - ci], 1u)] = w;
-            }
-        }
-        __syncthreads();
-        if (t == 0) ctl[ci] = 0u;
-        __syncthreads();
-        uint32_t *tmp = cur; cur = nxt; nxt = tmp;
-        ci = 3 - ci;
-    }
-    // keys: the level, or the cycle key after every level (max(largest level, 1) + 1)
-    const uint32_t maxl = ctl[3];
-    const uint32_t ck = (maxl > 1u ? maxl : 1u) + 1u;
-    uint32_t *start = fr0;  // both frontiers are free now: 2 V + 2 words for ck + 1 <= V + 2 bins
-    for (uint32_t k = t; k <= ck; k += blockDim.x) start[k] = 0u;
-    __syncthreads();
-    uint32_t nc = 0;
-    for (uint32_t v = t; v < V; v += blockDim.x) {
-        const bool cy = deg[v] != 0u;
-        nc += cy ? 1u : 0u;
-        atomicAdd(&start[cy ? ck : lvl[v]], 1u);
-    }
-    if (nc) atomicAdd(&ctl[4], nc);
-    __syncthreads();
-    if (t == 0) {  // exclusive scan of <= V + 1 bins (small)
-        uint32_t run = 0;
-        for (uint32_t k = 0; k <= ck; ++k) { const uint32_t x = start[k]; start[k] = run; run += x; }
-    }
-    __syncthreads();
-    // stable scatter in index order by one wave: equal keys ranked by a ballot match mask
-    if (t < 64) {
-        const uint32_t nbits = 32u - (uint32_t)__builtin_clz(ck);
-        const uint64_t lt = (1ull << lane) - 1ull;
-        for (uint32_t v0 = 0; v0 < V; v0 += 64) {
-            const uint32_t v = v0 + lane;
-            const bool valid = v < V;
-            const bool cy = valid && deg[v] != 0u;
-            const uint32_t k = valid ? (cy ? ck : lvl[v]) : 0u;
-            uint64_t m = __builtin_amdgcn_ballot_w64(valid);
-            for (uint32_t b = 0; b < nbits; ++b) {
-                const bool bit = (k >> b) & 1u;
-                const uint64_t bb = __builtin_amdgcn_ballot_w64(bit);
-                m &= bit ? bb : ~bb;
-            }
-            const uint32_t off = start[k];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane's read before the update
-            if (valid) {
-                if ((m & lt) == 0) start[k] = off + (uint32_t)__popcll(m);
-                order[off + (uint32_t)__popcll(m & lt)] = v;
-                level[v] = cy ? FP_NONE : lvl[v];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        }
-    }
-    if (t == 0 && ncyc_out) *ncyc_out = ctl[4];
+    if (threadIdx.x == 0 && ncyc_out) *ncyc_out = nc;
 }
 
 inline unsigned blocks_for(size_t n, unsigned b) {
@@ -945,7 +860,9 @@ static int level_sort(hipStream_t st, bool counting, uint32_t *keys, uint32_t *c
                       size_t sort_tmp, uint32_t *cs_hist) {
     const uint32_t ntiles = (uint32_t)(((size_t)V + CS_TILE - 1) / CS_TILE);
     if (counting && ntiles <= CS_MAX_TILES) {
-        const uint32_t passes = (fp_bitwidth((uint64_t)V + 1) + CS_BITS - 1) / CS_BITS;
+        // the largest key either schedule can produce: the async cycle key is max(level, 1) + 1 <=
+        // V + 1; the level-synchronous one is iters + 2 <= (V + 1) + 2: V + 3
+        const uint32_t passes = (fp_bitwidth((uint64_t)V + 3) + CS_BITS - 1) / CS_BITS;
         for (uint32_t p = 0; p < passes; ++p) {
             const uint32_t *ik = p ? kb[(p - 1) & 1] : keys;
             const uint32_t *iv = p ? vb[(p - 1) & 1] : nullptr;
@@ -1065,10 +982,14 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     }
     k_lvl_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, V, level, fa, &cnt[0]);
     FP_HIP(hipGetLastError());
-    // corrupt CSR => stop before expanding
+    // corrupt CSR => stop before expanding.  This call's own `bad` word decides (read back with the
+    // first frontier's size); the error itself stays in the kernel error word, reported like any
+    // other (fp_ctx_sync, or the host call's copy-back), and every later kernel of the call reads
+    // `bad` and does nothing -- a pending error of an earlier call is neither reported nor cleared
     FP_HIP(hipMemcpyAsync((char *)c->h_small + 8, &cnt[0], 4, hipMemcpyDeviceToHost, st));
-    if ((rc = fp_take_err(c))) return rc;
-    const uint32_t f0 = ((uint32_t *)c->h_small)[2];
+    FP_HIP(hipMemcpyAsync((char *)c->h_small + 12, bad, 4, hipMemcpyDeviceToHost, st));
+    FP_HIP(hipStreamSynchronize(st));
+    const uint32_t f0 = ((uint32_t *)c->h_small)[3] ? 0u : ((uint32_t *)c->h_small)[2];
     // Levels are enqueued in chunks of kChunk launches with no read-back in between
     // (a level whose frontier is empty is a no-op launch); one read of the last
     // chunk's final counter decides whether another chunk is needed.  The grid is

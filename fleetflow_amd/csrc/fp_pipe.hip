@@ -30,6 +30,7 @@
 #include "fp_pipe_sys.h"
 #include <stdlib.h>
 #include <string.h>
+#include <mutex>
 #include <type_traits>
 #include <utility>
 
@@ -1352,6 +1353,15 @@ struct PipeGeom {
     uint32_t sys_extra; // systolic steps past the queue length before the serial finish
 };
 
+// Per-device gate of bounded launches (fp_pipe_launch): the event the last bounded launch on the
+// device recorded on its stream, and the lock that orders the wait / launch / record of each.
+struct BoundedGate {
+    std::mutex m;
+    hipEvent_t ev = nullptr;
+};
+constexpr int kMaxGateDevices = 64;
+static BoundedGate g_bounded_gate[kMaxGateDevices];
+
 // Global link ring size when every segment of the launch is co-resident: 256 slots x 64
 // containers in flight per link (128 KB).  FP_OPT_LINK_SLOTS overrides (>= 8; tests force
 // small rings to exercise back-pressure).
@@ -1547,6 +1557,21 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     a.thr = thr;
     const bool wide = wide_g(W, G);
     if (G < 1 || (wide ? (G > MAX_G_WIDE || G % 4) : G > MAX_G)) return FP_EOVERFLOW;
+    // A bounded launch's producers wait on consumers of the same launch, so it needs its segments
+    // co-resident (pipe_geom: the batch fits the device, a scenario's chain twice over).  Another
+    // context's bounded launch on the same device could hold the slots it needs; bounded launches
+    // of this process are therefore serialised per device (BoundedGate): each waits, on its own
+    // stream, for the previous one to finish.  Unbounded launches never wait on a consumer and
+    // finish whatever else runs, so they only delay a bounded one, never block it.
+    std::unique_lock<std::mutex> gate_lock;
+    BoundedGate *gate = nullptr;
+    if (geo.bounded) {
+        if (c->device < 0 || c->device >= kMaxGateDevices) return FP_EINVAL;
+        gate = &g_bounded_gate[c->device];
+        gate_lock = std::unique_lock<std::mutex>(gate->m);
+        if (!gate->ev) FP_HIP(hipEventCreateWithFlags(&gate->ev, hipEventDisableTiming));
+        else FP_HIP(hipStreamWaitEvent(st, gate->ev, 0));
+    }
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
     int rc = (wide12_big(S, W, G) ? kLaunchWide12Big : wide ? kLaunchWide[G / 4] : kLaunch[G])(st, (unsigned)(S * B),
@@ -1554,6 +1579,10 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     if (rc) return rc;
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
+    if (gate) {
+        FP_HIP(hipEventRecord(gate->ev, st));
+        gate_lock.unlock();
+    }
     {
         const bool narrow16 = N < 0xFFFFu;  // node indices and FP_NONE (-> 0xFFFF) fit 16 bits
         const uint32_t span = narrow16 ? UNSORT_SPAN16 : UNSORT_SPAN32;

@@ -227,50 +227,72 @@ def _server_nodes(flow: Flow, servers: list[str]):
     return out
 
 
+def _stage_tables(names: list[str], flow: Flow, nodes: list[Server]):
+    """The stage's services (vertex order) and servers as the SoA tables of the C ABI: label,
+    host-port and anti-affinity bit dictionaries (SPEC.md 4)."""
+    svcs = [flow.services.get(n, Service()) for n in names]
+    all_labels = [lab for s in svcs for lab in s.labels] + [lab for nd in nodes for lab in nd.labels]
+    ld = LabelDict(all_labels)
+    ports = sorted({hp for s in svcs for hp in s.host_ports})
+    groups = sorted({s.anti_affinity for s in svcs if s.anti_affinity})
+    if len(ports) > 16 or len(groups) > 16:
+        raise ValueError("more than 16 host ports or anti-affinity groups in one stage")
+    pbit = {hp: i for i, hp in enumerate(ports)}
+    gbit = {g: 16 + i for i, g in enumerate(groups)}
+    cpu = [s.cpu_m for s in svcs]
+    mem = [s.mem_mib for s in svcs]
+    req = [ld.mask(s.labels) for s in svcs]
+    conf = []
+    for s in svcs:
+        m = 0
+        for hp in s.host_ports:
+            m |= 1 << pbit[hp]
+        if s.anti_affinity:
+            m |= 1 << gbit[s.anti_affinity]
+        conf.append(m)
+    cf = [nd.cpu_m for nd in nodes]
+    mf = [nd.mem_mib for nd in nodes]
+    lab = [ld.mask(nd.labels) for nd in nodes]
+    cu = [0] * len(nodes)
+    sch = [1 if nd.schedulable else 0 for nd in nodes]
+    return (cpu, mem, req, conf), (cf, mf, lab, cu, sch)
+
+
 def plan_stage(flow: Flow, stage_name: str, planner: Planner | None = None,
                servers: list[Server] | None = None) -> Plan:
-    """Full planner output for one stage (SPEC.md 2)."""
+    """Full planner output for one stage (SPEC.md 2): the `fleet up --dry-run`
+    plan (up.rs:57-136).  One fp_plan_stage call -- A1 order, A2 levels, and with servers the stage-2
+    candidates and the FFD plan -- when every service name appears once in the stage; a stage
+    listing a name twice (positions != vertices) takes the per-output calls."""
     p = planner or default_planner()
     stage = flow.stages[stage_name]
     services = list(stage.services)
-    order = order_by_dependencies(services, flow, p)
-    levels, level_order = levelize_stage(services, flow, p)
     nodes = servers if servers is not None else _server_nodes(flow, stage.servers)
     assignment, rejected, candidates = {}, {}, {}
-    if services and nodes:
-        names, pos2v, *_ = stage_graph(services, flow)
-        lvl_v = {names[v]: levels[i] for i, v in enumerate(pos2v)}
-        svcs = [flow.services.get(n, Service()) for n in names]
-        all_labels = [lab for s in svcs for lab in s.labels] + [lab for nd in nodes for lab in nd.labels]
-        ld = LabelDict(all_labels)
-        ports = sorted({hp for s in svcs for hp in s.host_ports})
-        groups = sorted({s.anti_affinity for s in svcs if s.anti_affinity})
-        if len(ports) > 16 or len(groups) > 16:
-            raise ValueError("more than 16 host ports or anti-affinity groups in one stage")
-        pbit = {hp: i for i, hp in enumerate(ports)}
-        gbit = {g: 16 + i for i, g in enumerate(groups)}
-        cpu = [s.cpu_m for s in svcs]
-        mem = [s.mem_mib for s in svcs]
-        req = [ld.mask(s.labels) for s in svcs]
-        conf = []
-        for s in svcs:
-            m = 0
-            for hp in s.host_ports:
-                m |= 1 << pbit[hp]
-            if s.anti_affinity:
-                m |= 1 << gbit[s.anti_affinity]
-            conf.append(m)
-        cf = [nd.cpu_m for nd in nodes]
-        mf = [nd.mem_mib for nd in nodes]
-        lab = [ld.mask(nd.labels) for nd in nodes]
-        cu = [0] * len(nodes)
-        sch = [1 if nd.schedulable else 0 for nd in nodes]
-        lv = [lvl_v[n] for n in names]
-        # stage 2 (fp_feasibility): feasible-server count and first feasible server per service
-        first, count, _ = p.feasibility((cpu, mem, req, conf), (cf, mf, lab, cu, sch), bitmap=False)
+    if not services:
+        return Plan(stage_name, [], {}, [], assignment, rejected, candidates)
+    names, pos2v, row_ptr, col, has_deps = stage_graph(services, flow)
+    if len(names) == len(services):
+        cont, ntab = _stage_tables(names, flow, nodes) if nodes else (None, None)
+        perm, level_v, order_v, _, placed = p.plan_stage(row_ptr, col, has_deps, cont, ntab)
+        order = [services[i] for i in perm]
+        levels = [int(x) for x in level_v]
+        level_order = [services[i] for i in order_v]
+    else:
+        order = order_by_dependencies(services, flow, p)
+        levels, level_order = levelize_stage(services, flow, p)
+        placed = None
+        if nodes:
+            lvl_v = {names[v]: levels[i] for i, v in enumerate(pos2v)}
+            cont, ntab = _stage_tables(names, flow, nodes)
+            # stage 2 (fp_feasibility): feasible-server count and first feasible server per service
+            first, count, _ = p.feasibility(cont, ntab, bitmap=False)
+            assign, reason, _ = p.place(cont, ntab, level=[lvl_v[n] for n in names])
+            placed = (first, count, assign, reason, None)
+    if placed is not None:
+        first, count, assign, reason, _ = placed
         candidates = {n: (int(count[v]), nodes[int(first[v])].slug if int(first[v]) != NONE else None)
                       for v, n in enumerate(names)}
-        assign, reason, _ = p.place((cpu, mem, req, conf), (cf, mf, lab, cu, sch), level=lv)
         for v, n in enumerate(names):
             if assign[v] != NONE:
                 assignment[n] = nodes[assign[v]].slug

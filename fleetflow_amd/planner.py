@@ -140,6 +140,40 @@ class Planner:
                                   order.ctypes.data_as(_lib.u32p), ct.byref(ncyc)), "fp_levelize")
         return level, order, ncyc.value
 
+    def plan_stage(self, row_ptr, col, has_deps, cont=None, nodes=None):
+        """fp_plan_stage: one stage's A1 legacy order, A2 levels and start order and, with ``nodes``
+        (container v = vertex v), the stage-2 candidates on the pristine table and the FFD plan gated
+        by the levels' CYCLE -- one call (one kernel for a fleet.kdl-sized stage).  Returns
+        (perm, level, order, n_cycle, placed) with placed = None or (first, count, assign, reason,
+        nodes_after)."""
+        rp, cl, hd = _u32(row_ptr), _u32(col), _u8(has_deps)
+        V = hd.size
+        perm = np.empty(V, np.uint32)
+        level = np.empty(V, np.uint32)
+        order = np.empty(V, np.uint32)
+        ncyc = ct.c_uint32()
+        g = FpGraph(V, cl.size, _ptr(rp), _ptr(cl) if cl.size else None, _ptr(hd))
+        u32 = _lib.u32p
+        if nodes is None:
+            check(self._L.fp_plan_stage(self._ctx, ct.byref(g), None, None, perm.ctypes.data_as(u32),
+                                        level.ctypes.data_as(u32), order.ctypes.data_as(u32), ct.byref(ncyc),
+                                        None, None, None, None), "fp_plan_stage")
+            return perm, level, order, ncyc.value, None
+        cpu, mem, req, conf = (_u32(x) for x in cont)
+        cf, mf = _u32(nodes[0]).copy(), _u32(nodes[1]).copy()
+        lab, cu, sched = _u32(nodes[2]), _u32(nodes[3]).copy(), _u8(nodes[4])
+        first = np.empty(V, np.uint32)
+        count = np.empty(V, np.uint32)
+        assign = np.empty(V, np.uint32)
+        reason = np.empty(V, np.uint8)
+        cs = FpContainers(V, _ptr(cpu), _ptr(mem), _ptr(req), _ptr(conf))
+        ns = FpNodes(cf.size, _ptr(cf), _ptr(mf), _ptr(lab), _ptr(cu), _ptr(sched))
+        check(self._L.fp_plan_stage(self._ctx, ct.byref(g), ct.byref(cs), ct.byref(ns), perm.ctypes.data_as(u32),
+                                    level.ctypes.data_as(u32), order.ctypes.data_as(u32), ct.byref(ncyc),
+                                    first.ctypes.data_as(u32), count.ctypes.data_as(u32), assign.ctypes.data_as(u32),
+                                    reason.ctypes.data_as(_lib.u8p)), "fp_plan_stage")
+        return perm, level, order, ncyc.value, (first, count, assign, reason, (cf, mf, lab, cu, sched))
+
     def place(self, cont, nodes, level=None):
         """cont = (cpu_m, mem_mib, req_labels, conflict); nodes = (cpu_free, mem_free,
         labels, conflict_used, schedulable).  Inputs are not mutated; the updated node
@@ -222,6 +256,12 @@ class Planner:
         """Stage 2 over every scenario of ``db`` ([S*C] outputs, scenario-major)."""
         self._dev(lambda: check(self._L.fp_dev_feasibility_batch(self._ctx, ct.byref(db.struct()), first_t.data_ptr(),
                                                                  count_t.data_ptr()), "fp_dev_feasibility_batch"))
+
+    def dev_legacy_order(self, has_deps_t, perm_t):
+        """fp_dev_legacy_order (engine.rs:67-85) on a device-resident has_deps vector."""
+        g = FpGraph(has_deps_t.numel(), 0, None, None, has_deps_t.data_ptr())
+        self._dev(lambda: check(self._L.fp_dev_legacy_order(self._ctx, ct.byref(g), perm_t.data_ptr()),
+                                "fp_dev_legacy_order"))
 
     def dev_levelize(self, row_ptr_t, col_t, has_deps_t, level_t, order_t, ncyc_t):
         V = has_deps_t.numel()

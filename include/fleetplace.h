@@ -36,10 +36,13 @@
  *     recorded on the old stream; the workspace is reused by every call).  It never
  *     touches the old stream handle itself, so a caller may destroy that stream once
  *     its own work on it is done.
- *   - The placement pipeline's bounded links (fp_place_geometry FP_GEOM_BOUNDED) assume
- *     the launch gets at least half of the device's resident workgroup slots; work of
- *     other processes crowding it out beyond that ends in FP_EDEVICE after the deadlock
- *     guard (60 s), never in a wrong plan.
+ *   - The placement pipeline's bounded links (fp_place_geometry FP_GEOM_BOUNDED) need the
+ *     launch's segments co-resident.  Bounded launches of one process are serialised per
+ *     device inside the library (each waits on its own stream for the previous one), so
+ *     contexts on several host threads may plan at once; other launches only delay them.
+ *     Only work of OTHER processes that holds the device's slots indefinitely can still
+ *     end a bounded launch in FP_EDEVICE after the deadlock guard (60 s), never in a
+ *     wrong plan.
  *   - Return 0 (FP_OK) or a negative FP_E* code.  There is no CPU fallback:
  *     fp_ctx_create fails with FP_EDEVICE when no MI355X (gfx950) is present.
  *   - One fp_ctx per host thread; contexts are not shared.
@@ -153,7 +156,8 @@ enum fp_option {
     FP_OPT_SPIN_TICKS = 7,    /* deadlock guard in 100 MHz ticks (auto: 60 s)               */
     FP_OPT_KPACK = 8,         /* 0 = bucket search per stage instead of packed buckets      */
     FP_OPT_SCEN_SORT = 9,     /* 0 = radix-key FFD order instead of the per-scenario LDS sort */
-    FP_OPT_SEGSORT = 10,      /* 0 = device-wide radix sort instead of segmented            */
+    FP_OPT_SEGSORT = 10,      /* ignored (kept for ABI stability): the radix path is always   */
+                              /* segmented for S > 1 and device-wide for S == 1             */
     FP_OPT_SYSTOLIC = 11,     /* systolic group fill for queues of >= value containers (0 = off) */
     FP_OPT_LEVELIZE_SYNC = 12,/* 1 = level-synchronous Kahn instead of the async levelizer */
     FP_OPT_SYSTOLIC_EXTRA = 13, /* systolic steps past the queue length before the serial finish */
@@ -184,6 +188,20 @@ int fp_place_batch(fp_ctx *ctx, const fp_batch *b);
  * bit (c, n) at word [(c/64) * N + n], bit c % 64. */
 int fp_feasibility(fp_ctx *ctx, const fp_containers *c, const fp_nodes *nodes,
                    uint32_t *first_out, uint32_t *count_out, uint64_t *bitmap_out);
+/* One stage's whole plan, the `fleet up --dry-run` path (crates/fleetflow/src/commands/up.rs:57-136):
+ *   perm_out                 A1 legacy start order (engine.rs:64-85, as fp_legacy_order)
+ *   level_out, order_out, n_cycle_out   A2 levels and start order (as fp_levelize)
+ * and, when nodes is not NULL (a stage with servers; c->n == n_vertices, container v = vertex v):
+ *   first_out, count_out     stage 2 on the pristine table (as fp_feasibility; nullable)
+ *   assign_out, reason_out   A6 first-fit-decreasing gated by the levels' CYCLE (as fp_place);
+ *                            nodes updated in place.
+ * A stage of <= 512 services, <= 8192 edges and <= 4096 servers is ONE kernel reading its inputs
+ * from and writing its results to mapped pinned host memory (one launch and one synchronisation,
+ * no copy calls: BASELINE config 1); larger stages run the general kernels.  FP_OPT_LEVEL_SMALL = 0
+ * forces the general path.  Synchronous; on error nothing is written. */
+int fp_plan_stage(fp_ctx *ctx, const fp_graph *g, const fp_containers *c, fp_nodes *nodes,
+                  uint32_t *perm_out, uint32_t *level_out, uint32_t *order_out, uint32_t *n_cycle_out,
+                  uint32_t *first_out, uint32_t *count_out, uint32_t *assign_out, uint8_t *reason_out);
 
 /* ---- device-pointer API (async on the ctx stream) ----------------------- */
 int fp_dev_legacy_order(fp_ctx *ctx, const fp_graph *g, uint32_t *perm_out);

@@ -8,7 +8,9 @@ use std::env;
 use std::path::PathBuf;
 use std::process::Command;
 
-const SOURCES: [&str; 6] = ["fp_ctx.hip", "fp_place.hip", "fp_pipe.hip", "fp_order.hip", "fp_feas.hip", "fp_gen.hip"];
+const SOURCES: [&str; 7] = [
+    "fp_ctx.hip", "fp_place.hip", "fp_pipe.hip", "fp_order.hip", "fp_feas.hip", "fp_gen.hip", "fp_small.hip",
+];
 
 fn main() {
     println!("cargo:rerun-if-env-changed=FLEETPLACE_LIB_DIR");
@@ -34,7 +36,7 @@ fn main() {
         println!("cargo:rerun-if-changed={}", p.display());
         cmd.arg(p);
     }
-    for h in ["fp_internal.h", "fp_pipe_asm.h", "../../include/fleetplace.h"] {
+    for h in ["fp_internal.h", "fp_pipe_asm.h", "fp_pipe_sys.h", "fp_pipe_sysv.h", "fp_small.h", "../../include/fleetplace.h"] {
         println!("cargo:rerun-if-changed={}", src.join(h).display());
     }
     let status = cmd.status().unwrap_or_else(|e| panic!("cannot run {hipcc}: {e} (set FLEETPLACE_LIB_DIR to a prebuilt libfleetplace.so)"));

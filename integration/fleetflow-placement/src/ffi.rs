@@ -31,6 +31,7 @@ pub const FP_OPT_PIPE_FLUSH: c_int = 6;
 pub const FP_OPT_SPIN_TICKS: c_int = 7;
 pub const FP_OPT_KPACK: c_int = 8;
 pub const FP_OPT_SCEN_SORT: c_int = 9;
+/// Ignored (kept for ABI stability): the radix path is segmented for S > 1, device-wide for S == 1.
 pub const FP_OPT_SEGSORT: c_int = 10;
 pub const FP_OPT_SYSTOLIC: c_int = 11;
 pub const FP_OPT_LEVELIZE_SYNC: c_int = 12;
@@ -133,6 +134,10 @@ unsafe extern "C" {
     pub fn fp_place_batch(ctx: *mut fp_ctx, b: *const fp_batch) -> c_int;
     pub fn fp_feasibility(ctx: *mut fp_ctx, c: *const fp_containers, nodes: *const fp_nodes, first_out: *mut u32,
                           count_out: *mut u32, bitmap_out: *mut u64) -> c_int;
+    pub fn fp_plan_stage(ctx: *mut fp_ctx, g: *const fp_graph, c: *const fp_containers, nodes: *mut fp_nodes,
+                         perm_out: *mut u32, level_out: *mut u32, order_out: *mut u32, n_cycle_out: *mut u32,
+                         first_out: *mut u32, count_out: *mut u32, assign_out: *mut u32, reason_out: *mut u8)
+                         -> c_int;
 
     pub fn fp_dev_legacy_order(ctx: *mut fp_ctx, g: *const fp_graph, perm_out: *mut u32) -> c_int;
     pub fn fp_dev_levelize(ctx: *mut fp_ctx, g: *const fp_graph, level_out: *mut u32, order_out: *mut u32,

@@ -5,4 +5,4 @@ set -e
 cd "$(dirname "$0")/../fleetflow_amd/csrc"
 suffix=$1; shift
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -munsafe-fp-atomics "$@" \
-  -shared -o ../libfleetplace$suffix.so fp_ctx.hip fp_place.hip fp_pipe.hip fp_order.hip fp_feas.hip fp_gen.hip
+  -shared -o ../libfleetplace$suffix.so fp_ctx.hip fp_place.hip fp_pipe.hip fp_order.hip fp_feas.hip fp_gen.hip fp_small.hip
