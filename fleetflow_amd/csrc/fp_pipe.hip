@@ -54,7 +54,7 @@ __device__ unsigned long long g_pipe_stats[16 * 16];
 #define STAT_GCLK() 0ull
 #define STAT_FINE 0
 #endif
-// per-batch timeline of scenario 0: [stage][batch] = (t_in_ready, t_prescan, t_cand, t_out_done)
+// per-batch timeline of scenario 0, global stages 0-15 (k_ffd_pipe: the record's fields)
 constexpr int TL_B = 2048;
 __device__ unsigned long long g_pipe_tl[16 * TL_B * 8];
 // per global stage of scenario 0 (s_memrealtime, 100 MHz, device-wide): [0] start [1] first
@@ -68,6 +68,16 @@ __device__ unsigned long long g_stage_span[SPAN_MAX * 8];
 #define STAT_GCLK() 0ull
 #define STAT_ON 0
 #define STAT_FINE 0
+#endif
+
+// Wave priority of the FFD stages (s_setprio, MI355X_MICROARCH.md "Two waves per SIMD" items 2 and 4):
+// 0 off; 1 raised to FP_PRIO_LEVEL while a wave runs its group loop (exact checks and fills, the
+// placement chain); 2 raised for a batch's whole work, lowered while the wave polls its input
+#ifndef FP_PRIO_MODE
+#define FP_PRIO_MODE 0
+#endif
+#ifndef FP_PRIO_LEVEL
+#define FP_PRIO_LEVEL 2
 #endif
 
 namespace fpp {
@@ -508,7 +518,12 @@ k_ffd_pipe(const PipeArgs a_arg) {
 #endif
     bool alive = true;
     while (alive) {
+        if (FP_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(0);  // polls / spins at the lowest priority
         ck_a = STAT_CLK();
+#ifdef FP_PIPE_STATS
+        const unsigned long long tl_top = ck_a;  // timeline: the previous batch's end
+        unsigned long long tl_avail = ck_a;      // timeline: this batch's input available
+#endif
         uint32_t cpu = 0, mem = 0, req = 0, conf = 0, idx = 0;
         bool valid = false;
         if (g_in) {
@@ -536,6 +551,9 @@ k_ffd_pipe(const PipeArgs a_arg) {
             }
             st_spin_in += n_sp;
             if (!got) break;
+#ifdef FP_PIPE_STATS
+            tl_avail = STAT_CLK();
+#endif
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
             // slots before itail are finished with: their loads returned last iteration
             // (the container fields they addressed were consumed), so the producer may
@@ -580,6 +598,9 @@ k_ffd_pipe(const PipeArgs a_arg) {
         } else {
             const uint32_t want = itail;
             if (!spin(&ictl[0], [want](uint32_t h) { return h != want; }, abort_flag, a.err, a.spin_ticks, st_spin_in)) break;
+#ifdef FP_PIPE_STATS
+            tl_avail = STAT_CLK();
+#endif
             const uint32_t slot = itail % R;
             const uint32_t n = ictl[2 + slot];
             if (n & END) break;
@@ -610,6 +631,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             kc = bucket_of(cpu, my_t, 0);
             km = bucket_of(mem, my_t, K);
         }
+        if (FP_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);  // the batch's work
         ck_b = STAT_CLK(); ck_in += ck_b - ck_a; ck_a = ck_b;
 #ifdef FP_PIPE_STATS
         if (!sp_first) sp_first = __builtin_amdgcn_s_memrealtime();
@@ -682,11 +704,13 @@ k_ffd_pipe(const PipeArgs a_arg) {
             // without the update, while config 4's 20-group stages need it (57 vs 66 ms)
             uint32_t nchk = 0, nhit = 0;
             unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
+            if (FP_PRIO_MODE == 1 && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
             if (todo)
                 fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
                                        __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
+            if (FP_PRIO_MODE == 1 && todo) __builtin_amdgcn_s_setprio(0);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
             if (STAT_FINE) { ck_gx += gst[0]; ck_gu += gst[1]; st_queues += (uint32_t)gst[2]; st_touched += (uint32_t)gst[3]; }
         }
@@ -711,10 +735,13 @@ k_ffd_pipe(const PipeArgs a_arg) {
         }
 #ifdef FP_PIPE_STATS
         if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B && b * W + w < 16) {
-            // global stage b * W + w; per batch: ready, prescan end, loop end, checks, hits, todo
+            // global stage b * W + w; per batch (s_memtime): [0] loop top (= the previous batch's end)
+            // [1] input available [2] input read [3] prescan end [4] group loop end, then [5] checks
+            // [6] hits [7] todo | valid << 32
             unsigned long long *tl = &g_pipe_tl[((size_t)(b * W + w) * TL_B + tl_idx) * 8];
-            tl[0] = ck_t0_batch; tl[1] = tl_pre; tl[2] = tl_cand;
-            tl[3] = st_checks - tl_checks0; tl[4] = st_hits - tl_hits0; tl[5] = tl_todo;
+            tl[0] = tl_top; tl[1] = tl_avail; tl[2] = ck_t0_batch; tl[3] = tl_pre; tl[4] = tl_cand;
+            tl[5] = st_checks - tl_checks0; tl[6] = st_hits - tl_hits0;
+            tl[7] = tl_todo | ((unsigned long long)__popcll(vm) << 32);
         }
 #endif
         const bool fwd = valid && !((placed >> lane) & 1ull);

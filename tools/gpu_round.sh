@@ -2,7 +2,7 @@
 # One GPU session: error-path tests (isolated, short limit), the -m gpu suite, the bench
 # (config 4 at 4096 + config 3 leg + CPU baseline), then the rocprofv3 passes.
 # Usage: tools/gpu_round.sh <tag> [steps...]
-#   steps: errors tests bench scale prof kt lvl sortstats pipestats model (default: errors tests bench prof)
+#   steps: errors tests bench scale prof kt lvl sortstats pipestats model front ab (default: errors tests bench prof)
 #   kt = config-4 kernel trace (tools/ktrace.sh), lvl = config-5 levelizer timing + kernel stats
 #   (tools/gpu_lvl.sh), sortstats / pipestats / model = diagnostics-build runs (k_scen_sort phases,
 #   per-stage pipeline counters at 4096 scenarios, the latency model of tools/pipe_model.py)
@@ -47,6 +47,21 @@ for s in $steps; do
       cat ${log}_pipestats.txt ;;
     model)
       timeout -k 10 400 python -u tools/pipe_model.py ${log}_pipe_model.json > ${log}_pipe_model.log 2>&1 || { echo "model failed"; tail ${log}_pipe_model.log; exit 1; } ;;
+    front)
+      # where a placement's cycles go at the front (diagnostics build timeline, tools/front_breakdown.py):
+      # config 3 and the 512-scenario per-rank load
+      SEED=0x5EED0003 C=1000000 N=100000 TIMELINE=${log}_tl_c3.csv timeout -k 10 300 python -u tools/pipe_stats.py 1 \
+        > ${log}_front_c3.txt 2>&1 || { echo "front c3 failed"; tail ${log}_front_c3.txt; exit 1; }
+      TIMELINE=${log}_tl_512.csv timeout -k 10 300 python -u tools/pipe_stats.py 512 \
+        > ${log}_front_512.txt 2>&1 || { echo "front 512 failed"; tail ${log}_front_512.txt; exit 1; }
+      python tools/front_breakdown.py ${log}_tl_c3.csv >> ${log}_front_c3.txt
+      python tools/front_breakdown.py ${log}_tl_512.csv >> ${log}_front_512.txt
+      tail -25 ${log}_front_c3.txt; tail -25 ${log}_front_512.txt ;;
+    ab)
+      # library variants on device-resident loads: AB_LIBS="- _suffix ...", AB_LOADS=c4x4096,c3,...
+      tools/ab_variants.sh $tag "${AB_LIBS:--}" ${AB_LOADS:-c4x4096,c3} > ${log}_ab.txt 2>&1 \
+        || { echo "ab failed"; tail -20 ${log}_ab.txt; exit 1; }
+      cat ${log}_ab.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -64,7 +64,9 @@ def main():
 
 
 def timeline(out_path):
-    """Dump scenario 0's per-batch timeline (stats build) to out_path as CSV (global stage = segment * W + stage)."""
+    """Dump scenario 0's per-batch timeline (stats build) to out_path as CSV (global stage = segment * W + stage):
+    s_memtime stamps of the loop top (= the previous batch's end), input available, input read, prescan end and
+    group loop end, then checks, hits, todo and the batch's valid containers (tools/front_breakdown.py)."""
     L = _lib.load()
     f = L.fp_debug_pipe_timeline
     f.argtypes = [ct.POINTER(ct.c_ulonglong)]
@@ -72,12 +74,12 @@ def timeline(out_path):
     buf = (ct.c_ulonglong * (16 * TLB * 8))()
     f(buf)
     with open(out_path, "w") as fo:
-        fo.write("stage,batch,t_ready,t_prescan,t_cand,checks,hits,todo\n")
+        fo.write("stage,batch,t_top,t_avail,t_in,t_pre,t_cand,checks,hits,todo,valid\n")
         for w in range(16):
             for b in range(TLB):
-                v = [buf[(w * TLB + b) * 8 + i] for i in range(6)]
+                v = [buf[(w * TLB + b) * 8 + i] for i in range(8)]
                 if v[0]:
-                    fo.write(f"{w},{b}," + ",".join(str(x) for x in v) + "\n")
+                    fo.write(f"{w},{b}," + ",".join(str(x) for x in v[:7]) + f",{v[7] & 0xFFFFFFFF},{v[7] >> 32}\n")
 
 
 def stage_span(out_path):

@@ -65,7 +65,11 @@ def main():
                     ref = (db.assign.clone(), db.cost.clone())
                 else:
                     same = bool(torch.equal(ref[0], db.assign) and torch.equal(ref[1], db.cost))
-                print(json.dumps({"load": load, "S": S, "C": C, "N": N, "opt": args.opt, "value": v,
+                # plan digest: equal across library variants when their plans are (tools/ab_variants.sh)
+                wts = torch.arange(db.assign.numel(), device=dev, dtype=torch.int64) % 65521 + 1
+                digest = int((db.assign.to(torch.int64) * wts).sum().item()) ^ int(db.cost.sum().item())
+                del wts
+                print(json.dumps({"load": load, "S": S, "C": C, "N": N, "opt": args.opt, "value": v, "digest": digest,
                                   "ffd_ms": round(statistics.median(times), 3),
                                   "wall_ms": round(statistics.median(walls), 3), "same_plan": same,
                                   "geometry": p.geometry(S, C, N)}), flush=True)
