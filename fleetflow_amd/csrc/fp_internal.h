@@ -55,6 +55,10 @@ struct fp_ctx {
     char *h_map = nullptr;
     void *d_map = nullptr;
     size_t h_map_cap = 0;
+    // the asynchronous levelizer's work queues (fp_order.hip), kept between calls: a clean finish
+    // leaves them empty, and the flag in their last 256 bytes tells the next call whether to refill
+    void *lvl_q = nullptr;
+    size_t lvl_q_cap = 0;
     // profiling
     bool profile = false;
     struct Rec { int kid; hipEvent_t a, b; };

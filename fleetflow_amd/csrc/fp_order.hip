@@ -258,70 +258,111 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // several levels in one round trip: each level is the previous + 1, no atomic on any of them,
 // and the rest of each passed vertex's edges goes to the queue as a partial item.  A chain of
 // depth D takes ~D / kHops rounds.  (Two levels per round: config-5 levelize 1.51 -> 1.13 ms.)
-__global__ void k_edge_rec(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t E,
-                           uint32_t V, const uint32_t *__restrict__ indeg, uint4 *__restrict__ rec,
-                           const uint32_t *__restrict__ bad) {
-    if (*bad) return;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t w = col[e];
-        rec[e] = w < V ? make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u)
-                       : make_uint4(w, 0u, 0u, 0u);  // corrupt: k_indeg raised FP_ECORRUPT, no expansion runs
-    }
+
+// ---- the async path's set-up in three launches (round 5; was 12 launches and memsets) ----------
+// The work queues (kShards x V u64, 64 MB at config 5) live in a context buffer of their own
+// (fp_ctx::lvl_q): k_lvl_async resets every slot it consumes, so a levelization that finishes
+// cleanly leaves them empty and marks the buffer clean (qflag = kQClean); the next call fills them
+// with kQEmpty only when the flag says otherwise (a fresh buffer, an aborted or corrupt call).
+constexpr uint32_t kQClean = 0x600Du;
+
+// in-degrees, the call's counters, the control words and the caller's n_cycle word zeroed; the
+// queues emptied when dirty
+__global__ void k_lvl_zero(uint32_t V, uint32_t *__restrict__ indeg, uint32_t *__restrict__ ncyc,
+                           uint32_t *__restrict__ actl, uint32_t *__restrict__ ncyc_out, uint4 *__restrict__ Q4,
+                           size_t q4, const uint32_t *__restrict__ qflag) {
+    const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = i0; i < V; i += st) indeg[i] = 0u;
+    if (i0 < 16) ncyc[i0] = 0u;
+    for (size_t i = i0; i < kCtlWords; i += st) actl[i] = 0u;
+    if (i0 == 0 && ncyc_out) *ncyc_out = 0u;
+    if (*qflag != kQClean)
+        for (size_t i = i0; i < q4; i += st) Q4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
 }
 
-// Hop h + 1 of every edge by pointer jumping over the finished records: the hop after edge e's
-// child w is the record of w's first edge (rec[rec[e].y]), and hop h + 1 of e is hop h of that
-// first edge -- one dependent 16-B load per edge and hop, instead of chasing col / row_ptr.
-// A hop is kept only while every edge before it is an only-parent edge (zero record otherwise).
-__global__ void k_edge_hop(uint32_t E, const uint4 *__restrict__ rec, const uint4 *__restrict__ prev,
-                           uint4 *__restrict__ next, const uint32_t *__restrict__ bad) {
-    if (*bad) return;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
-        const uint4 r = rec[e];
-        const uint4 p = prev ? prev[e] : r;  // the hop before (the child itself for the first hop)
-        uint4 n = make_uint4(0u, 0u, 0u, 0u);
-        if (p.w != 0u && r.w != 0u && r.z > r.y && r.y < E) {
-            const uint4 f = prev ? prev[r.y] : rec[r.y];  // hop (h) of the child's first edge
-            if (f.w != 0u) n = f;
+// the CSR check (k_check_csr's conditions) and the in-degrees (k_indeg) in one pass; marks the
+// queues dirty until k_lvl_async finishes cleanly
+__global__ void k_indeg_check(const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t V,
+                              uint32_t E, uint32_t *__restrict__ indeg, uint32_t *__restrict__ err,
+                              uint32_t *__restrict__ bad, uint32_t *__restrict__ qflag) {
+    const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
+    if (i0 == 0) {
+        *qflag = 0u;
+        if (row_ptr[0] != 0 || row_ptr[V] != E) lv_corrupt(err, bad);
+    }
+    const size_t n = V > E ? V : E;
+    for (size_t i = i0; i < n; i += st) {
+        if (i < V && row_ptr[i + 1] < row_ptr[i]) lv_corrupt(err, bad);
+        if (i < E) {
+            const uint32_t v = col[i];
+            if (v >= V) lv_corrupt(err, bad);
+            else atomicAdd(&indeg[v], 1u);
         }
-        next[e] = n;
     }
 }
 
-__global__ void k_lvl_async_init(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
-                                 const uint32_t *__restrict__ row_ptr, uint32_t V, uint32_t *__restrict__ level,
-                                 uint64_t *__restrict__ state, uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
-                                 bool pk, const uint32_t *__restrict__ bad) {
+// k_lvl_async_init (blocks [0, vblocks): one vertex per thread) beside the edge records and their
+// hops (the other blocks, grid-stride over the edges): k_edge_rec's record of edge e and
+// k_edge_hop's kHops - 1 hops, each hop computed from col / row_ptr / indeg by chasing first edges
+// (hop h + 1 of e = the record of the first edge of hop h's vertex, kept while every edge on the
+// way is its child's only in-edge) -- one launch for what took five
+__global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
+                           const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t V,
+                           uint32_t E, uint32_t vblocks, uint32_t *__restrict__ level, uint64_t *__restrict__ state,
+                           uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl, bool pk, uint4 *__restrict__ rec,
+                           uint4 *__restrict__ rec2, const uint32_t *__restrict__ bad) {
     if (*bad) return;
-    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool in = v < V;
-    uint32_t l0 = 0, deg = 0;
-    bool src = false;
-    if (in) {
-        l0 = hd[v] ? 1u : 0u;
-        deg = row_ptr[v + 1] - row_ptr[v];
-        src = indeg[v] == 0;
-        state[v] = ((uint64_t)l0 << 32) | indeg[v];
-        level[v] = src && deg == 0 ? l0 : FP_NONE;
+    if (blockIdx.x < vblocks) {
+        const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const bool in = v < V;
+        uint32_t l0 = 0, deg = 0;
+        bool src = false;
+        if (in) {
+            l0 = hd[v] ? 1u : 0u;
+            deg = row_ptr[v + 1] - row_ptr[v];
+            src = indeg[v] == 0;
+            state[v] = ((uint64_t)l0 << 32) | indeg[v];
+            level[v] = src && deg == 0 ? l0 : FP_NONE;
+        }
+        const bool push = src && deg != 0;
+        const uint64_t m = __ballot(push);
+        if (!m) return;
+        const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(m);
+        const uint32_t sh = (uint32_t)((v >> 6) % kShards);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&ctl[(kShards + sh) * kCtlStride], (uint32_t)__popcll(m));
+        base = __shfl(base, (int)leader);
+        if (push)
+            Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
+                ((uint64_t)(pk ? l0 << 8 : l0) << 32) | v;
+        return;
     }
-    const bool push = src && deg != 0;
-    const uint64_t m = __ballot(push);
-    if (!m) return;
-    const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(m);
-    const uint32_t sh = (uint32_t)((v >> 6) % kShards);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&ctl[(kShards + sh) * kCtlStride], (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader);
-    if (push)
-        Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
-            ((uint64_t)(pk ? l0 << 8 : l0) << 32) | v;
+    const size_t st = (size_t)(gridDim.x - vblocks) * blockDim.x;
+    for (size_t e = (size_t)(blockIdx.x - vblocks) * blockDim.x + threadIdx.x; e < E; e += st) {
+        const uint32_t w = col[e];  // < V: k_indeg_check raised `bad` otherwise
+        const uint4 r = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
+        rec[e] = r;
+        uint4 cur = r;
+        bool ok = r.w != 0u;
+#pragma unroll
+        for (uint32_t h = 0; h + 1 < kHops; ++h) {
+            uint4 nx = make_uint4(0u, 0u, 0u, 0u);
+            if (ok && cur.z > cur.y && cur.y < E) {
+                const uint32_t w2 = col[cur.y];
+                if (w2 < V && indeg[w2] == 1u) nx = make_uint4(w2, row_ptr[w2], row_ptr[w2 + 1], 1u);
+            }
+            rec2[(size_t)h * E + e] = nx;
+            ok = nx.w != 0u;
+            cur = nx;
+        }
+    }
 }
 
 __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
                                                   const uint4 *__restrict__ erec2, uint32_t E, uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
                                                   uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
                                                   uint32_t *__restrict__ err, bool pk,
-                                                  const uint32_t *__restrict__ bad) {
+                                                  const uint32_t *__restrict__ bad, uint32_t *__restrict__ qflag) {
     if (*bad) return;  // a corrupt CSR: no expansion (uniform: every block leaves)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sh = blockIdx.x % kShards;
@@ -514,6 +555,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             }
         }
         if (x != kQEmpty) {
+            // the slot is consumed: empty it again, so that a clean finish leaves the queues empty
+            // for the next call (kQClean)
+            __hip_atomic_store(const_cast<uint64_t *>(&q[slot]), kQEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             has_claim = false;
             has_item = true;
             u = (uint32_t)x;
@@ -598,6 +642,7 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                 for (uint32_t k = 0; k < kShards; ++k) t += ag_rmw_rd(&ctl[(kShards + k) * kCtlStride]);
                 if (d == t) {
                     __hip_atomic_store(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (qflag) __hip_atomic_store(qflag, kQClean, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     stop = 1;
                 }
             }
@@ -624,7 +669,7 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
 __global__ void k_lvl_async_final(uint32_t V, const uint32_t *__restrict__ ctl, const uint32_t *__restrict__ level,
                                   uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t *__restrict__ ncyc,
                                   uint32_t *__restrict__ ck,
-                                  const uint32_t *__restrict__ bad) {
+                                  const uint32_t *__restrict__ bad, uint32_t *__restrict__ ncyc_out) {
     if (*bad) return;
     const uint32_t maxl = ctl[26 * kCtlStride];
     const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
@@ -636,7 +681,10 @@ __global__ void k_lvl_async_final(uint32_t V, const uint32_t *__restrict__ ctl, 
         vals[v] = (uint32_t)v;  // the radix fallback's values (the counting sort's scratch)
     }
     const uint64_t m = __ballot(cyc);
-    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(ncyc, (uint32_t)__popcll(m));
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) {
+        atomicAdd(ncyc, (uint32_t)__popcll(m));
+        if (ncyc_out) atomicAdd(ncyc_out, (uint32_t)__popcll(m));
+    }
 }
 
 // ---- stable counting sort of the level keys (the start order) ----------------------------
@@ -909,7 +957,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
     }
-    const size_t async_ws = level_sync ? 0 : (size_t)V * 8 * (1 + kShards) + (size_t)E * 16 * kHops + kCtlWords * 4;
+    const size_t async_ws = level_sync ? 0 : (size_t)V * 8 + (size_t)E * 16 * kHops + kCtlWords * 4;
     const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 : 0;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + async_ws + cs_ws + 23 * 256);
     if (rc) return rc;
@@ -933,8 +981,57 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     uint32_t *const kb[2] = {keys_out, fa}, *const vb[2] = {fb, vals};  // sort scratch; vals = identity
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_LEVEL, &ev);
+    if (!level_sync) {
+        if ((uint64_t)V + 65536ull * 64 >= 0xFFFFFFFFull) return FP_EOVERFLOW;  // queue heads stay below 2^32
+        uint64_t *state = (uint64_t *)fp_ws_take(c, (size_t)V * 8);
+        uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
+        uint4 *erec = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
+        uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16 * (kHops - 1)) : nullptr;
+        if (!state || !actl || (E && (!erec || !erec2))) return FP_ENOMEM;
+        // the queues: the context's own buffer, emptied by the device only when dirty (kQClean)
+        const size_t qbytes = (size_t)V * 8 * kShards;
+        if (qbytes + 256 > c->lvl_q_cap) {
+            FP_HIP(hipStreamSynchronize(st));
+            if (c->lvl_q) (void)hipFree(c->lvl_q);
+            c->lvl_q = nullptr;
+            c->lvl_q_cap = 0;
+            const size_t cap = (qbytes + qbytes / 4 + 4096 + 255) & ~(size_t)255;
+            FP_HIP(hipMalloc(&c->lvl_q, cap));
+            c->lvl_q_cap = cap;
+            FP_HIP(hipMemsetAsync((char *)c->lvl_q + cap - 256, 0, 256, st));  // flag: dirty
+        }
+        uint64_t *Q = (uint64_t *)c->lvl_q;
+        uint32_t *qflag = (uint32_t *)((char *)c->lvl_q + c->lvl_q_cap - 256);
+        // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
+        const bool pk = V < (1u << 24);
+        const unsigned zg = blocks_for(qbytes / 16, 256) < 8192 ? blocks_for(qbytes / 16, 256) : 8192;
+        k_lvl_zero<<<zg, 256, 0, st>>>(V, indeg, ncyc, actl, n_cycle_dev, (uint4 *)Q, qbytes / 16, qflag);
+        FP_HIP(hipGetLastError());
+        const size_t nmax = V + 1 > E ? (size_t)V + 1 : E;
+        k_indeg_check<<<blocks_for(nmax, 256) < 8192 ? blocks_for(nmax, 256) : 8192, 256, 0, st>>>(
+            g->row_ptr, g->col, V, E, indeg, c->d_err, bad, qflag);
+        FP_HIP(hipGetLastError());
+        const uint32_t vblocks = blocks_for(V, 256);
+        const unsigned eg = E ? (blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192) : 0u;
+        k_lvl_prep<<<vblocks + eg, 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, g->col, V, E, vblocks, level, state, Q,
+                                                 actl, pk, erec, erec2, bad);
+        FP_HIP(hipGetLastError());
+        if (E) {
+            // one wave per block, kAsyncBlocks of them
+            k_lvl_async<<<kAsyncBlocks, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err,
+                                                     pk, bad, qflag);
+            FP_HIP(hipGetLastError());
+        }
+        // the cycle key (from the largest level seen) is computed on the device: no read-back; the
+        // cycle count goes straight to the caller's word (zeroed by k_lvl_zero)
+        k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, actl, level, keys, vals, ncyc, ck, bad, n_cycle_dev);
+        FP_HIP(hipGetLastError());
+        if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
+        fp_prof_end(c, FP_K_LEVEL, ev);
+        return FP_OK;
+    }
     FP_HIP(hipMemsetAsync(indeg, 0, (size_t)V * 4, st));
-    if (level_sync) FP_HIP(hipMemsetAsync(cnt, 0, ncnt * 4, st));  // the per-level frontier counts
+    FP_HIP(hipMemsetAsync(cnt, 0, ncnt * 4, st));  // the per-level frontier counts
     FP_HIP(hipMemsetAsync(ncyc, 0, 64, st));
     k_check_csr<<<blocks_for(V, 256), 256, 0, st>>>(g->row_ptr, V, E, c->d_err, bad);
     FP_HIP(hipGetLastError());
@@ -942,43 +1039,6 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         k_indeg<<<blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192, 256, 0, st>>>(
             g->col, E, V, indeg, c->d_err, bad);
         FP_HIP(hipGetLastError());
-    }
-    if (!level_sync) {
-        if ((uint64_t)V + 65536ull * 64 >= 0xFFFFFFFFull) return FP_EOVERFLOW;  // queue heads stay below 2^32
-        uint64_t *state = (uint64_t *)fp_ws_take(c, (size_t)V * 8);
-        uint64_t *Q = (uint64_t *)fp_ws_take(c, (size_t)V * 8 * kShards);
-        uint32_t *actl = (uint32_t *)fp_ws_take(c, kCtlWords * 4);
-        uint4 *erec = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16) : nullptr;
-        uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16 * (kHops - 1)) : nullptr;
-        if (!state || !Q || !actl || (E && (!erec || !erec2))) return FP_ENOMEM;
-        FP_HIP(hipMemsetAsync(Q, 0xFF, (size_t)V * 8 * kShards, st));
-        FP_HIP(hipMemsetAsync(actl, 0, kCtlWords * 4, st));
-        // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
-        const bool pk = V < (1u << 24);
-        k_lvl_async_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, V, level, state, Q, actl,
-                                                             pk, bad);
-        FP_HIP(hipGetLastError());
-        if (E) {
-            const unsigned eg = blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192;
-            k_edge_rec<<<eg, 256, 0, st>>>(g->row_ptr, g->col, E, V, indeg, erec, bad);
-            FP_HIP(hipGetLastError());
-            for (uint32_t h = 0; h + 1 < kHops; ++h) {
-                k_edge_hop<<<eg, 256, 0, st>>>(E, erec, h ? erec2 + (size_t)(h - 1) * E : nullptr, erec2 + (size_t)h * E,
-                                               bad);
-                FP_HIP(hipGetLastError());
-            }
-            // one wave per block, kAsyncBlocks of them
-            k_lvl_async<<<kAsyncBlocks, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err,
-                                                     pk, bad);
-            FP_HIP(hipGetLastError());
-        }
-        // the cycle key (from the largest level seen) is computed on the device: no read-back
-        k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, actl, level, keys, vals, ncyc, ck, bad);
-        FP_HIP(hipGetLastError());
-        if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
-        if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
-        fp_prof_end(c, FP_K_LEVEL, ev);
-        return FP_OK;
     }
     k_lvl_init<<<blocks_for(V, 256), 256, 0, st>>>(g->has_deps, indeg, V, level, fa, &cnt[0]);
     FP_HIP(hipGetLastError());

@@ -70,12 +70,12 @@ __device__ unsigned long long g_stage_span[SPAN_MAX * 8];
 #define STAT_FINE 0
 #endif
 
-// Wave priority of the FFD stages (s_setprio, MI355X_MICROARCH.md "Two waves per SIMD" items 2 and 4):
-// 0 off; 1 raised to FP_PRIO_LEVEL while a wave runs its group loop (exact checks and fills, the
-// placement chain); 2 raised for a batch's whole work, lowered while the wave polls its input
-#ifndef FP_PRIO_MODE
-#define FP_PRIO_MODE 0
-#endif
+// Wave priority of the FFD stages (s_setprio, MI355X_MICROARCH.md "Two waves per SIMD" items 2 and 4),
+// PipeArgs::prio: 0 off; 1 raised to FP_PRIO_LEVEL while a wave runs its group loop (exact checks and
+// fills: the placement chain); 2 raised for a batch's whole work, lowered while the wave polls its
+// input.  r05a A/B (profiles/r05a_prio_ab.jsonl, FFD ms): 512 config-4 scenarios 6.96-7.00 -> 6.20-6.30
+// (mode 1) / 6.61-6.68 (mode 2); config 3 64.8-65.0 -> 63.6-63.8 / 64.6-65.0; 4096 scenarios
+// 15.06-15.08 -> 15.16-15.19 / 15.03: mode 1 except for the throughput kernel (wide12_big)
 #ifndef FP_PRIO_LEVEL
 #define FP_PRIO_LEVEL 2
 #endif
@@ -125,6 +125,7 @@ struct PipeArgs {
     uint32_t *err;
     uint64_t spin_ticks;    // deadlock guard, s_memrealtime ticks (100 MHz)
     const uint32_t *thr;    // [2K] device: ascending thresholds, cpu then mem, thr[0] = thr[K] = 0
+    uint32_t prio;          // wave priority mode (FP_PRIO_LEVEL comment)
 };
 
 __device__ __forceinline__ uint32_t lds_acq(uint32_t *p) {
@@ -374,7 +375,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
     const PipeArgs &a = a_arg;  // the host pass only type-checks the body
 #endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t W = a.W, R = a.R, B = a.B;
+    const uint32_t W = a.W, R = a.R, B = a.B, prio = a.prio;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t C = a.C, N = a.N;
@@ -518,7 +519,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
 #endif
     bool alive = true;
     while (alive) {
-        if (FP_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(0);  // polls / spins at the lowest priority
+        if (prio == 2u) __builtin_amdgcn_s_setprio(0);  // polls / spins at the lowest priority
         ck_a = STAT_CLK();
 #ifdef FP_PIPE_STATS
         const unsigned long long tl_top = ck_a;  // timeline: the previous batch's end
@@ -631,7 +632,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             kc = bucket_of(cpu, my_t, 0);
             km = bucket_of(mem, my_t, K);
         }
-        if (FP_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);  // the batch's work
+        if (prio == 2u) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);  // the batch's work
         ck_b = STAT_CLK(); ck_in += ck_b - ck_a; ck_a = ck_b;
 #ifdef FP_PIPE_STATS
         if (!sp_first) sp_first = __builtin_amdgcn_s_memrealtime();
@@ -704,13 +705,13 @@ k_ffd_pipe(const PipeArgs a_arg) {
             // without the update, while config 4's 20-group stages need it (57 vs 66 ms)
             uint32_t nchk = 0, nhit = 0;
             unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
-            if (FP_PRIO_MODE == 1 && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
+            if (prio == 1u && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
             if (todo)
                 fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
                                        __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
-            if (FP_PRIO_MODE == 1 && todo) __builtin_amdgcn_s_setprio(0);
+            if (prio == 1u && todo) __builtin_amdgcn_s_setprio(0);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
             if (STAT_FINE) { ck_gx += gst[0]; ck_gu += gst[1]; st_queues += (uint32_t)gst[2]; st_touched += (uint32_t)gst[3]; }
         }
@@ -1378,6 +1379,7 @@ struct PipeGeom {
     uint32_t resident;  // workgroups of this kernel resident on the device at once (0: unknown)
     uint32_t sys;       // systolic group fill for queues of >= sys containers (0: off)
     uint32_t sys_extra; // systolic steps past the queue length before the serial finish
+    uint32_t prio;      // wave priority mode (PipeArgs::prio)
 };
 
 // Per-device gate of bounded launches (fp_pipe_launch): the event the last bounded launch on the
@@ -1462,6 +1464,10 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
     if (g->sys_extra > 128) g->sys_extra = 128;
     if (fp_opt(c, FP_OPT_SYSTOLIC_VALU, 0) != 0) g->sys_extra |= 0x8000u;  // fp_pipe_sysv.h step loop
+    {
+        const int64_t pv = fp_opt(c, FP_OPT_PIPE_PRIO, wide12_big(S, W, G) ? 0 : 1);
+        g->prio = pv >= 0 && pv <= 2 ? (uint32_t)pv : 0u;
+    }
     return true;
 }
 
@@ -1582,6 +1588,7 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     // bucket thresholds (device; fp_place.hip k_thresholds chooses them -- any ascending choice
     // with T0 = 0 is exact, it only decides how tight the candidate masks are)
     a.thr = thr;
+    a.prio = geo.prio;
     const bool wide = wide_g(W, G);
     if (G < 1 || (wide ? (G > MAX_G_WIDE || G % 4) : G > MAX_G)) return FP_EOVERFLOW;
     // A bounded launch's producers wait on consumers of the same launch, so it needs its segments

@@ -20,6 +20,8 @@ def _plan_loop(case, reps, out, barrier):
     from fleetflow_amd import Planner
     try:
         with Planner(0) as p:
+            for k, v in case.get("opts", {}).items():
+                p.set_option(k, v)
             cont, nodes = case["cont"], case["nodes"]
             out["geometry"] = p.geometry(1, cont[0].size, nodes[0].size)
             barrier.wait(timeout=60)
@@ -34,9 +36,12 @@ def test_two_contexts_bounded_at_once(O):
         "nodes100k": O.gen_scenario(SEED + 3, 0, 120_000, 100_000, 7),
     }
     reps = {"config2": 12, "nodes100k": 3}
+    # config 2's 159-slot links already hold every container: 16-slot rings make it bounded too
+    opts = {"config2": {"link_slots": 16}, "nodes100k": {}}
     outs = {k: {} for k in cases}
     barrier = threading.Barrier(len(cases))
-    threads = [threading.Thread(target=_plan_loop, args=({"cont": c, "nodes": n}, reps[k], outs[k], barrier))
+    threads = [threading.Thread(target=_plan_loop, args=({"cont": c, "nodes": n, "opts": opts[k]}, reps[k], outs[k],
+                                                              barrier))
                for k, (c, n) in cases.items()]
     for t in threads:
         t.start()

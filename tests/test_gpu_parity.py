@@ -767,3 +767,50 @@ def test_scen_sort_mixed_eligibility(planner, O):
         assert np.array_equal(reason[s * C:(s + 1) * C], er), s
         assert int(cost[s]) == O.cost(ea, N, 40 + s)
         assert np.array_equal(after[0][s * N:(s + 1) * N], eafter[0])
+
+
+@pytest.mark.parametrize("V", [1021, 1022, 1025])
+def test_levelize_sync_cycle_key_pass_boundary(V, planner, O):
+    """The level-synchronous schedule's cycle key is iters + 2 <= V + 3: at V = 1021 /
+    1022 a chain as deep as the graph makes it 1024 / 1025 -- 11 bits, two counting-sort passes, so
+    the queued pass count must cover V + 3.  The general path (> 512 vertices), both schedules."""
+    edges = [(v, v + 1) for v in range(V - 1)]
+    rp, col = _csr(V, edges)
+    hd = np.ones(V, np.uint8)
+    el, eo, en = O.levelize(rp, col, hd)
+    for sync in (1, 0):
+        planner.set_option("levelize_sync", sync)
+        try:
+            level, order, ncyc = planner.levelize(rp, col, hd)
+        finally:
+            planner.set_option("levelize_sync")
+        assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
+def test_levelize_queue_reuse_across_calls(planner, O):
+    """The asynchronous levelizer keeps its work queues between calls and refills them only when
+    the last call left them dirty (fp_order.hip kQClean): alternate graphs, a corrupt CSR (queues
+    dirty), an edgeless graph (no async kernel) and bigger graphs (the buffer grows), every result
+    against the oracle."""
+    from fleetflow_amd._lib import FleetplaceError
+
+    def dag(V, E, seed):
+        rng = np.random.default_rng(seed)
+        a, b = rng.integers(0, V, E), rng.integers(0, V, E)
+        edges = [(int(x), int(y)) for x, y in zip(a, b) if x < y] + [(V - 3, V - 2), (V - 2, V - 1), (V - 1, V - 3)]
+        rp, col = _csr(V, edges)
+        hd = (rng.random(V) < 0.7).astype(np.uint8)
+        return rp, col, hd
+
+    graphs = [dag(5_000, 20_000, 1), dag(40_000, 90_000, 2), "corrupt", dag(5_000, 20_000, 1),
+              (np.zeros(2_001, np.uint32), np.zeros(0, np.uint32), np.ones(2_000, np.uint8)),
+              dag(120_000, 300_000, 3), dag(40_000, 90_000, 2)]
+    for g in graphs:
+        if isinstance(g, str):  # "corrupt": col out of range
+            with pytest.raises(FleetplaceError):
+                planner.levelize([0, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2] + [2] * 600, [1, 5000], np.ones(610, np.uint8))
+            continue
+        rp, col, hd = g
+        level, order, ncyc = planner.levelize(rp, col, hd)
+        el, eo, en = O.levelize(rp, col, hd)
+        assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en

@@ -5,7 +5,9 @@ Per batch i of a stage: wait = input available - loop top (spinning on the upstr
 input = read done - available, prescan = prescan end - read done, group = group loop end - prescan end
 (exact checks, systolic fill, re-tests, mask upkeep), forward = next loop top - group loop end
 (assignment stores, forwarding, output-ring waits).  "Filling" batches place >= FILL of their valid
-containers: the stage is then the front (its group fills for the stream's current sizes).
+containers (and hold >= 32): the stage is then the front (its group fills for the stream's current sizes);
+the wait before the first batch of a run of filling batches is the front's travel to the stage, not
+counted.
 
     python tools/front_breakdown.py tl.csv [clock_ghz] [FILL]"""
 import json
@@ -26,7 +28,11 @@ def breakdown(path, ghz=2.4, fill=0.25):
         ph = pd.DataFrame({"wait": g.t_avail - g.t_top, "input": g.t_in - g.t_avail, "prescan": g.t_pre - g.t_in,
                            "group": g.t_cand - g.t_pre, "forward": nxt - g.t_cand})
         ok = nxt.notna() & (g.valid > 0)
-        front = ok & (g.hits >= fill * g.valid) & (g.hits > 0)
+        front = ok & (g.hits >= fill * g.valid) & (g.hits > 0) & (g.valid >= 32)
+        # a run of filling batches: the wait before its first batch is the time the front took to
+        # reach this stage, not a stall of the fill
+        first_of_run = front & ~front.shift(1, fill_value=False)
+        ph.loc[first_of_run, "wait"] = 0
         h = int(g.hits[front].sum())
         rec = {"batches": int(ok.sum()), "front_batches": int(front.sum()), "front_hits": h,
                "hits_all": int(g.hits.sum()), "checks_front": int(g.checks[front].sum())}
