@@ -62,6 +62,12 @@ for s in $steps; do
       tools/ab_variants.sh $tag "${AB_LIBS:--}" ${AB_LOADS:-c4x4096,c3} > ${log}_ab.txt 2>&1 \
         || { echo "ab failed"; tail -20 ${log}_ab.txt; exit 1; }
       cat ${log}_ab.txt ;;
+    sweep)
+      # one context option over device-resident loads: SWEEP_OPT, SWEEP_VALUES, SWEEP_LOADS (tools/sys_sweep.py)
+      timeout -k 10 400 python -u tools/sys_sweep.py --opt ${SWEEP_OPT:?} --values ${SWEEP_VALUES:?} \
+        --loads ${SWEEP_LOADS:-c4x512,c3} --reps 3 ${SWEEP_SET:+--set $SWEEP_SET} > ${log}_sweep_${SWEEP_OPT}.jsonl 2>&1 \
+        || { echo "sweep failed"; tail -20 ${log}_sweep_${SWEEP_OPT}.jsonl; exit 1; }
+      cut -c1-200 ${log}_sweep_${SWEEP_OPT}.jsonl | grep load ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

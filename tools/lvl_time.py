@@ -17,5 +17,5 @@ with Planner(0) as p:
         k, v = kv.split("=")
         p.set_option(k, int(v))
     for _ in range(2):
-        lv, _, _, _ = bench.levelize_leg(p, torch.device("cuda", 0), 10)
+        lv = bench.levelize_leg(p, torch.device("cuda", 0), 10)[0]
         print(json.dumps({k: lv[k] for k in ("ms_per_step", "kernel_ms", "levels", "cycle_vertices")}), flush=True)
