@@ -259,7 +259,7 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // and the rest of each passed vertex's edges goes to the queue as a partial item.  A chain of
 // depth D takes ~D / kHops rounds.  (Two levels per round: config-5 levelize 1.51 -> 1.13 ms.)
 
-// ---- the async path's set-up in three launches (round 5; was 12 launches and memsets) ----------
+// ---- the async path's set-up in four launches (round 5; was 12 launches and memsets) -----------
 // The work queues (kShards x V u64, 64 MB at config 5) live in a context buffer of their own
 // (fp_ctx::lvl_q): k_lvl_async resets every slot it consumes, so a levelization that finishes
 // cleanly leaves them empty and marks the buffer clean (qflag = kQClean); the next call fills them
@@ -301,16 +301,13 @@ __global__ void k_indeg_check(const uint32_t *__restrict__ row_ptr, const uint32
     }
 }
 
-// k_lvl_async_init (blocks [0, vblocks): one vertex per thread) beside the edge records and their
-// hops (the other blocks, grid-stride over the edges): k_edge_rec's record of edge e and
-// k_edge_hop's kHops - 1 hops, each hop computed from col / row_ptr / indeg by chasing first edges
-// (hop h + 1 of e = the record of the first edge of hop h's vertex, kept while every edge on the
-// way is its child's only in-edge) -- one launch for what took five
+// The vertex states and the source queue items (blocks [0, vblocks): one vertex per thread) beside
+// the edge records (the other blocks, grid-stride over the edges) in one launch
 __global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
                            const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t V,
                            uint32_t E, uint32_t vblocks, uint32_t *__restrict__ level, uint64_t *__restrict__ state,
                            uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl, bool pk, uint4 *__restrict__ rec,
-                           uint4 *__restrict__ rec2, const uint32_t *__restrict__ bad) {
+                           const uint32_t *__restrict__ bad) {
     if (*bad) return;
     if (blockIdx.x < vblocks) {
         const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -340,16 +337,29 @@ __global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__res
     const size_t st = (size_t)(gridDim.x - vblocks) * blockDim.x;
     for (size_t e = (size_t)(blockIdx.x - vblocks) * blockDim.x + threadIdx.x; e < E; e += st) {
         const uint32_t w = col[e];  // < V: k_indeg_check raised `bad` otherwise
-        const uint4 r = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
-        rec[e] = r;
-        uint4 cur = r;
-        bool ok = r.w != 0u;
+        rec[e] = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
+    }
+}
+
+// The kernel after k_lvl_prep: the kHops - 1 hops of every edge whose child has it as its only
+// in-edge, by chasing the finished records along first edges (hop h + 1 of e = the record of the
+// first edge of hop h's vertex, kept while every edge on the way is its child's only in-edge).
+// k_lvl_async reads an edge's hops only when the edge itself is an only-parent edge (rec.w), so the
+// hops of the other edges are left unwritten.  (Chasing col / row_ptr / indeg inside k_lvl_prep
+// instead: 0.121 ms against 0.07, profiles/r05b_lvl_kernel_stats.csv.)
+__global__ void k_edge_hops(uint32_t E, const uint4 *__restrict__ rec, uint4 *__restrict__ rec2,
+                            const uint32_t *__restrict__ bad) {
+    if (*bad) return;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        uint4 cur = rec[e];
+        if (cur.w == 0u) continue;
+        bool ok = true;
 #pragma unroll
         for (uint32_t h = 0; h + 1 < kHops; ++h) {
             uint4 nx = make_uint4(0u, 0u, 0u, 0u);
             if (ok && cur.z > cur.y && cur.y < E) {
-                const uint32_t w2 = col[cur.y];
-                if (w2 < V && indeg[w2] == 1u) nx = make_uint4(w2, row_ptr[w2], row_ptr[w2 + 1], 1u);
+                const uint4 f = rec[cur.y];
+                if (f.w != 0u) nx = f;
             }
             rec2[(size_t)h * E + e] = nx;
             ok = nx.w != 0u;
@@ -1014,9 +1024,13 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         const uint32_t vblocks = blocks_for(V, 256);
         const unsigned eg = E ? (blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192) : 0u;
         k_lvl_prep<<<vblocks + eg, 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, g->col, V, E, vblocks, level, state, Q,
-                                                 actl, pk, erec, erec2, bad);
+                                                 actl, pk, erec, bad);
         FP_HIP(hipGetLastError());
         if (E) {
+            if (pk) {  // the hops are read only with packed queue entries
+                k_edge_hops<<<eg, 256, 0, st>>>(E, erec, erec2, bad);
+                FP_HIP(hipGetLastError());
+            }
             // one wave per block, kAsyncBlocks of them
             k_lvl_async<<<kAsyncBlocks, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err,
                                                      pk, bad, qflag);

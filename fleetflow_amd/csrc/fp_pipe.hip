@@ -730,10 +730,10 @@ k_ffd_pipe(const PipeArgs a_arg) {
         const unsigned long long tl_cand = ck_b;
         const uint32_t tl_idx = st_batches - 1;
 #endif
-        if ((placed >> lane) & 1ull) {
-            a.assign[cb + (idx & pmask)] = my_assign;
-            a.reason[cb + (idx & pmask)] = FP_REASON_OK;
-        }
+        // a placed container's reason is OK by definition: k_unsort derives it from the assignment, so
+        // the pipeline stores only the node (reasons are written for the unplaced: CYCLE / screened
+        // NOFIT in segment 0, NOFIT at the last stage)
+        if ((placed >> lane) & 1ull) a.assign[cb + (idx & pmask)] = my_assign;
 #ifdef FP_PIPE_STATS
         if (s == 0 && lane == 0 && tl_idx < (uint32_t)TL_B && b * W + w < 16) {
             // global stage b * W + w; per batch (s_memtime): [0] loop top (= the previous batch's end)
@@ -1240,7 +1240,8 @@ __global__ __launch_bounds__(1024) void k_unsort(uint32_t C, uint32_t H, uint32_
         for (uint32_t u = 0; u < U; ++u) {
             if (j[u] >= lo && j[u] < hi) {
                 la[j[u] - lo] = (A)av[u];  // FP_NONE -> 0xFFFF when narrow
-                lr[j[u] - lo] = rv[u];
+                // placed: OK (the pipeline writes no reason for a placed container)
+                lr[j[u] - lo] = av[u] != FP_NONE ? (uint8_t)FP_REASON_OK : rv[u];
             }
         }
     }

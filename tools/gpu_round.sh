@@ -57,6 +57,12 @@ for s in $steps; do
       python tools/front_breakdown.py ${log}_tl_c3.csv >> ${log}_front_c3.txt
       python tools/front_breakdown.py ${log}_tl_512.csv >> ${log}_front_512.txt
       tail -25 ${log}_front_c3.txt; tail -25 ${log}_front_512.txt ;;
+    tl4096)
+      # config 4's per-batch timeline (diagnostics build; scenario 0's segments = global stages 0-6)
+      TIMELINE=${log}_tl_4096.csv timeout -k 10 300 python -u tools/pipe_stats.py 4096 \
+        > ${log}_tl4096.txt 2>&1 || { echo "tl4096 failed"; tail ${log}_tl4096.txt; exit 1; }
+      python tools/front_breakdown.py ${log}_tl_4096.csv 2.4 0 >> ${log}_tl4096.txt
+      tail -30 ${log}_tl4096.txt ;;
     ab)
       # library variants on device-resident loads: AB_LIBS="- _suffix ...", AB_LOADS=c4x4096,c3,...
       tools/ab_variants.sh $tag "${AB_LIBS:--}" ${AB_LOADS:-c4x4096,c3} > ${log}_ab.txt 2>&1 \
@@ -64,7 +70,7 @@ for s in $steps; do
       cat ${log}_ab.txt ;;
     sweep)
       # one context option over device-resident loads: SWEEP_OPT, SWEEP_VALUES, SWEEP_LOADS (tools/sys_sweep.py)
-      timeout -k 10 400 python -u tools/sys_sweep.py --opt ${SWEEP_OPT:?} --values ${SWEEP_VALUES:?} \
+      timeout -k 10 400 python -u tools/sys_sweep.py --opt ${SWEEP_OPT:?} --values=${SWEEP_VALUES:?} \
         --loads ${SWEEP_LOADS:-c4x512,c3} --reps 3 ${SWEEP_SET:+--set $SWEEP_SET} > ${log}_sweep_${SWEEP_OPT}.jsonl 2>&1 \
         || { echo "sweep failed"; tail -20 ${log}_sweep_${SWEEP_OPT}.jsonl; exit 1; }
       cut -c1-200 ${log}_sweep_${SWEEP_OPT}.jsonl | grep load ;;
