@@ -1464,7 +1464,12 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     if (g->sys > 64) g->sys = 64;
     g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
     if (g->sys_extra > 128) g->sys_extra = 128;
-    if (fp_opt(c, FP_OPT_SYSTOLIC_VALU, 0) != 0) g->sys_extra |= 0x8000u;  // fp_pipe_sysv.h step loop
+    {  // step loop: 0 exec-masked (fp_pipe_sys.h), 1 VALU-only (fp_pipe_sysv.h), 2 DPP-folded (fp_pipe_sysd.h,
+       // the default: 109-123 vs 134-153 cycles per container in tools/ubench/systolic.hip, r05e)
+        const int64_t sv = fp_opt(c, FP_OPT_SYSTOLIC_VALU, 2);
+        if (sv == 1) g->sys_extra |= 0x8000u;
+        else if (sv == 2) g->sys_extra |= 0x4000u;
+    }
     {
         const int64_t pv = fp_opt(c, FP_OPT_PIPE_PRIO, wide12_big(S, W, G) ? 0 : 1);
         g->prio = pv >= 0 && pv <= 2 ? (uint32_t)pv : 0u;

@@ -228,6 +228,7 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
 }  // namespace fpp
 
 #include "fp_pipe_sysv.h"
+#include "fp_pipe_sysd.h"
 
 namespace fpp {
 
@@ -244,9 +245,12 @@ __device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint
     // `extra`: steps the systolic phase runs past the queue length before the serial loop
     // takes the containers still open (PipeArgs::sys_extra)
     // extra bit 15: the VALU-only step loop (fp_pipe_sysv.h, FP_OPT_SYSTOLIC_VALU)
-    const uint32_t cap = (uint32_t)__builtin_popcountll(q) + (extra & 0x7FFFu);
+    // extra bit 14: the DPP-folded step loop (fp_pipe_sysd.h, FP_OPT_SYSTOLIC_VALU = 2)
+    const uint32_t cap = (uint32_t)__builtin_popcountll(q) + (extra & 0x3FFFu);
     const SysOut so = (extra & 0x8000u)
                           ? fpp_sysv_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap)
+                      : (extra & 0x4000u)
+                          ? fpp_sysd_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap)
                           : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap);
     uint64_t left = fpp_uniform64(so.left);
     touched = fpp_uniform64(touched);

@@ -163,7 +163,7 @@ enum fp_option {
     FP_OPT_SYSTOLIC_EXTRA = 13, /* systolic steps past the queue length before the serial finish */
     FP_OPT_SCREEN = 14,       /* 0 = no stage-2 early-NOFIT screen: every container enters    */
     FP_OPT_PAYLOAD_LDS = 15,  /* 0 = random-gather payload instead of the LDS-chunked one      */
-    FP_OPT_SYSTOLIC_VALU = 16,/* 1 = VALU-only systolic steps (fp_pipe_sysv.h), 0 = exec-masked  */
+    FP_OPT_SYSTOLIC_VALU = 16,/* systolic step loop: 0 exec-masked, 1 VALU-only, auto/2 DPP-folded */
     FP_OPT_LINK_PUBLISH = 17, /* full slots per head publish on unbounded global links (auto 32) */
     FP_OPT_LEVEL_SORT = 18,   /* levelizer start order: 0 = radix sort, auto = LSD counting sort   */
     FP_OPT_LEVEL_SMALL = 19,  /* 0 = no one-launch levelizer (<= 512 vertices) / legacy order (<= 1024) */

@@ -111,7 +111,7 @@ def test_geometry_query_defaults(planner):
 
 
 # ---- systolic group fill (fp_pipe_sys.h) ------------------------------------------------------
-@pytest.mark.parametrize("valu", [0, 1])
+@pytest.mark.parametrize("valu", [0, 1, 2])
 @pytest.mark.parametrize("thr", [1, 24])
 @pytest.mark.parametrize("C,N,flags,w,seg", [(20_000, 6_000, 7, 4, 4), (60_000, 12_000, 7, 4, 4),
                                              (4_000, 641, 7, 1, 12), (5_000, 5_121, 3, 1, 32),
@@ -134,7 +134,7 @@ def test_systolic_fill_vs_oracle(C, N, flags, w, seg, thr, valu, planner, O, opt
         assert np.array_equal(after[i], eafter[i])
 
 
-@pytest.mark.parametrize("valu", [0, 1])
+@pytest.mark.parametrize("valu", [0, 1, 2])
 @pytest.mark.parametrize("thr", [1, 16])
 def test_systolic_batch_zero_and_cycles(thr, valu, planner, O, opts):
     """Systolic fill in a many-scenario batch with all-zero containers, cycles and cordoned

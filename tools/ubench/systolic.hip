@@ -15,6 +15,7 @@
 #include "fp_pipe_asm.h"
 #include "fp_pipe_sys.h"
 #include "fp_pipe_sysv.h"
+#include "fp_pipe_sysd.h"
 
 using namespace fpp;
 
@@ -81,9 +82,10 @@ __global__ void k_sys(uint64_t *out, uint32_t *res, int pattern, uint32_t reps, 
             fpp_group_x<0, 1>(q, placed, touched, asg, nxt, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 1u, 0u, 0u, nchk,
                               nhit, qc, qm);
         } else {
-            const uint32_t cap = (V == 1 || V == 3) ? 1000u : (uint32_t)__builtin_popcountll(q) + extra;
-            SysOut so = V >= 3 ? fpp_sysv_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm, cap)
-                               : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm, cap);
+            const uint32_t cap = (V == 1 || V == 3 || V == 5) ? 1000u : (uint32_t)__builtin_popcountll(q) + extra;
+            SysOut so = V >= 5   ? fpp_sysd_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm, cap)
+                        : V >= 3 ? fpp_sysv_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm, cap)
+                                 : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, qc, qm, cap);
             uint64_t left = __builtin_amdgcn_readfirstlane((uint32_t)so.left) |
                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(so.left >> 32)) << 32);
             if (left) fpp_asm_group_x<false>(left, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 0u, nchk);
@@ -110,13 +112,14 @@ int main() {
     hipMalloc(&d, 64 * 8);
     hipMalloc(&dr, 5 * 64 * 4);
     const uint32_t reps = 64;
-    const char *names[] = {"serial exec-masked (fpp_group_x)", "systolic, full", "systolic, Q+extra + serial",
-                           "VALU systolic, full", "VALU systolic, Q+extra + serial"};
+    const char *names[7] = {"serial exec-masked (fpp_group_x)", "systolic, full", "systolic, Q+extra + serial",
+                           "VALU systolic, full", "VALU systolic, Q+extra + serial", "DPP-folded systolic, full",
+                           "DPP-folded, Q+extra + serial"};
     for (int pattern : {0, 1, 2, 3, 4}) {
         uint32_t ref[320], got[320];
-        for (int v = 0; v <= 4; ++v) {
-            for (uint32_t extra : {0u, 8u, 24u}) {
-                if ((v < 2 || v == 3) && extra) continue;
+        for (int v = 0; v <= 6; ++v) {
+            for (uint32_t extra : {0u, 8u, 16u}) {
+                if ((v < 2 || v == 3 || v == 5) && extra) continue;
                 for (int nw : {1, 4}) {
                     uint64_t h[64] = {0};
                     for (int it = 0; it < 2; ++it) {
@@ -125,7 +128,9 @@ int main() {
                         else if (v == 1) k_sys<1><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         else if (v == 2) k_sys<2><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         else if (v == 3) k_sys<3><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
-                        else k_sys<4><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else if (v == 4) k_sys<4><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else if (v == 5) k_sys<5><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else k_sys<6><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
                         hipMemcpy(h, d, 64 * 8, hipMemcpyDeviceToHost);
                     }
