@@ -131,14 +131,20 @@ __device__ __forceinline__ SysOut fpp_sysd_group(uint64_t q, uint64_t &touched, 
     }
     const bool inq = (q >> lane) & 1ull;
     const uint32_t Q = (uint32_t)__builtin_popcountll(q);
-    const uint32_t rq = inq ? (uint32_t)__builtin_popcountll(q & below) : Q + (uint32_t)__builtin_popcountll(~q & below);
-    const uint32_t kc = sys_push(rq, cpu), km = sys_push(rq, mem), kr = sys_push(rq, req), kx = sys_push(rq, conf);
+    // a queue that is lanes 0..Q-1 (a batch arriving whole at a filling group) is compacted already,
+    // and a group whose nodes are all live needs no position map: no permutes for either
+    const bool qpre = (q & (q + 1ull)) == 0ull, lfull = lm == ~0ull;
+    const uint32_t rq = qpre ? lane
+                        : inq ? (uint32_t)__builtin_popcountll(q & below)
+                              : Q + (uint32_t)__builtin_popcountll(~q & below);
+    uint32_t kc = cpu, km = mem, kr = req, kx = conf;
+    if (!qpre) { kc = sys_push(rq, cpu); km = sys_push(rq, mem); kr = sys_push(rq, req); kx = sys_push(rq, conf); }
     const bool live = (lm >> lane) & 1ull;
     const uint32_t pos = live ? (uint32_t)__builtin_popcountll(lm & below) : L + (uint32_t)__builtin_popcountll(~lm & below);
     // position p starts at lane (63 - p) & 63: one rotation behind the first step (see above)
     const uint32_t at0 = (63u - pos) & 63u;
     uint32_t xc = sys_push(at0, rcf), xm = sys_push(at0, rmf), xu = sys_push(at0, rcu), xl = sys_push(at0, rlab);
-    const uint32_t pmap = sys_push(pos, lane);
+    const uint32_t pmap = lfull ? lane : sys_push(pos, lane);
     if (((63u - lane) & 63u) >= L) {  // filler positions fit nothing
         xc = 0u; xm = 0u; xu = 0xFFFFFFFFu; xl = 0xFFFFFFFFu;
     }
@@ -150,11 +156,11 @@ __device__ __forceinline__ SysOut fpp_sysd_group(uint64_t q, uint64_t &touched, 
     const uint32_t src = (tau - 1u - pos) & 63u;
     const uint32_t ncf = sys_pull(src, xc), nmf = sys_pull(src, xm), ncu = sys_pull(src, xu);
     if (live) { rcf = ncf; rmf = nmf; rcu = ncu; }
-    const uint32_t nl = sys_pull(apos & 63u, pmap);
+    const uint32_t nl = lfull ? (apos & 63u) : sys_pull(apos & 63u, pmap);
     const uint32_t cnode = apos != 0xFFFFFFFFu ? gbg + nl : 0xFFFFFFFFu;
-    const uint32_t back = sys_pull(rq, cnode);
+    const uint32_t back = qpre ? cnode : sys_pull(rq, cnode);
     const uint32_t open = k < L ? 1u : 0u;
-    const uint32_t open_here = sys_pull(rq, open);
+    const uint32_t open_here = qpre ? open : sys_pull(rq, open);
     if (inq) asg = back;
     out.left = __builtin_amdgcn_ballot_w64(inq && open_here != 0);
     const uint32_t bl = apos != 0xFFFFFFFFu && nl < 32 ? 1u << nl : 0u;
