@@ -878,6 +878,15 @@ k_ffd_pipe(const PipeArgs a_arg) {
             lds_rel(&octl[0], ohead);
         }
     }
+    if (G == 1) {
+        // one-group stages: the systolic fill does not track the nodes it placed on; a placement of a
+        // container with any nonzero field changes its node's record (capacity only shrinks, and a
+        // conflict bit must be new to fit), and all-zero containers set usedbits above
+        const uint32_t n = gbase * 64 + lane;
+        if (n < N && (schedbits & 1u) &&
+            (a.cf[nb + n] != rcf[0] || a.mf[nb + n] != rmf[0] || a.cu[nb + n] != rcu[0]))
+            usedbits |= 1u;
+    }
     {  // nodes of this stage that received a container
         uint32_t u = (uint32_t)__popc(usedbits) + (uint32_t)__popc(used_hi);
 #pragma unroll

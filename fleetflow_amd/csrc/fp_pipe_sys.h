@@ -250,7 +250,9 @@ __device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint
     const SysOut so = (extra & 0x8000u)
                           ? fpp_sysv_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap)
                       : (extra & 0x4000u)
-                          ? fpp_sysd_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap)
+                          // one-group stages take their used nodes from the final records (k_ffd_pipe)
+                          ? fpp_sysd_group<(G > 1)>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc,
+                                                    qm, cap)
                           : fpp_sys_group(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, qc, qm, cap);
     uint64_t left = fpp_uniform64(so.left);
     touched = fpp_uniform64(touched);

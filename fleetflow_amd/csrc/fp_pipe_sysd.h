@@ -115,7 +115,9 @@ __device__ __forceinline__ uint32_t fpp_sysd_steps(uint32_t &xc, uint32_t &xm, u
     return tau;
 }
 
-// fpp_sys_group with the DPP-folded step loop (same contract).
+// fpp_sys_group with the DPP-folded step loop (same contract).  TOUCHED = false: `touched` is left
+// alone (one-group stages derive their used nodes from the final records, k_ffd_pipe).
+template <bool TOUCHED = true>
 __device__ __forceinline__ SysOut fpp_sysd_group(uint64_t q, uint64_t &touched, uint32_t &asg, uint32_t &rcf,
                                                  uint32_t &rmf, uint32_t &rcu, uint32_t rlab, uint32_t cpu,
                                                  uint32_t mem, uint32_t req, uint32_t conf, uint32_t gbg, uint32_t qc,
@@ -163,9 +165,11 @@ __device__ __forceinline__ SysOut fpp_sysd_group(uint64_t q, uint64_t &touched, 
     const uint32_t open_here = qpre ? open : sys_pull(rq, open);
     if (inq) asg = back;
     out.left = __builtin_amdgcn_ballot_w64(inq && open_here != 0);
-    const uint32_t bl = apos != 0xFFFFFFFFu && nl < 32 ? 1u << nl : 0u;
-    const uint32_t bh = apos != 0xFFFFFFFFu && nl >= 32 ? 1u << (nl - 32) : 0u;
-    touched |= ((uint64_t)sys_wave_or(bh) << 32) | sys_wave_or(bl);
+    if (TOUCHED) {
+        const uint32_t bl = apos != 0xFFFFFFFFu && nl < 32 ? 1u << nl : 0u;
+        const uint32_t bh = apos != 0xFFFFFFFFu && nl >= 32 ? 1u << (nl - 32) : 0u;
+        touched |= ((uint64_t)sys_wave_or(bh) << 32) | sys_wave_or(bl);
+    }
     return out;
 }
 
