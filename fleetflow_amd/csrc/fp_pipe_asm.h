@@ -161,9 +161,10 @@ __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64
     (void)nhit;
 #endif
     placed |= hit;
-    if (inq && asg == 0xFFFFFFFFu) {
+    {  // the misses move on to their next candidate group (a select: no divergent branch)
         const uint64_t above = (((uint64_t)cand_hi << 32) | cand) & ~((2ull << g) - 1ull);
-        nxt = above ? (uint32_t)__builtin_ctzll(above) : G;
+        const uint32_t nx = above ? (uint32_t)__builtin_ctzll(above) : G;
+        nxt = (inq && asg == 0xFFFFFFFFu) ? nx : nxt;
     }
 }
 

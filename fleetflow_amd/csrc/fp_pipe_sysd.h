@@ -123,7 +123,6 @@ __device__ __forceinline__ SysOut fpp_sysd_group(uint64_t q, uint64_t &touched, 
                                                  uint32_t mem, uint32_t req, uint32_t conf, uint32_t gbg, uint32_t qc,
                                                  uint32_t qm, uint32_t max_steps) {
     const uint32_t lane = __lane_id();
-    const uint64_t below = (1ull << lane) - 1ull;
     SysOut out{0};
     const uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
     const uint32_t L = (uint32_t)__builtin_popcountll(lm);
@@ -134,22 +133,26 @@ __device__ __forceinline__ SysOut fpp_sysd_group(uint64_t q, uint64_t &touched, 
     const bool inq = (q >> lane) & 1ull;
     const uint32_t Q = (uint32_t)__builtin_popcountll(q);
     // a queue that is lanes 0..Q-1 (a batch arriving whole at a filling group) is compacted already,
-    // and a group whose nodes are all live needs no position map: no permutes for either
+    // and a group whose nodes are all live needs no position map: no permutes for either.  The ranks
+    // are branch-free (v_mbcnt + one select): per-lane ternaries over two popcounts compiled to
+    // divergent branches
     const bool qpre = (q & (q + 1ull)) == 0ull, lfull = lm == ~0ull;
-    const uint32_t rq = qpre ? lane
-                        : inq ? (uint32_t)__builtin_popcountll(q & below)
-                              : Q + (uint32_t)__builtin_popcountll(~q & below);
+    const uint32_t qa = __builtin_amdgcn_mbcnt_hi((uint32_t)(q >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)q, 0u));
+    const uint32_t rq = qpre ? lane : inq ? qa : Q + lane - qa;
     uint32_t kc = cpu, km = mem, kr = req, kx = conf;
     if (!qpre) { kc = sys_push(rq, cpu); km = sys_push(rq, mem); kr = sys_push(rq, req); kx = sys_push(rq, conf); }
     const bool live = (lm >> lane) & 1ull;
-    const uint32_t pos = live ? (uint32_t)__builtin_popcountll(lm & below) : L + (uint32_t)__builtin_popcountll(~lm & below);
+    const uint32_t la = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+    const uint32_t pos = live ? la : L + lane - la;
     // position p starts at lane (63 - p) & 63: one rotation behind the first step (see above)
     const uint32_t at0 = (63u - pos) & 63u;
     uint32_t xc = sys_push(at0, rcf), xm = sys_push(at0, rmf), xu = sys_push(at0, rcu), xl = sys_push(at0, rlab);
     const uint32_t pmap = lfull ? lane : sys_push(pos, lane);
-    if (((63u - lane) & 63u) >= L) {  // filler positions fit nothing
-        xc = 0u; xm = 0u; xu = 0xFFFFFFFFu; xl = 0xFFFFFFFFu;
-    }
+    const bool filler = ((63u - lane) & 63u) >= L;  // filler positions fit nothing
+    xc = filler ? 0u : xc;
+    xm = filler ? 0u : xm;
+    xu = filler ? 0xFFFFFFFFu : xu;
+    xl = filler ? 0xFFFFFFFFu : xl;
     uint32_t k = lane < Q ? (0u - lane) : 0x80000000u;
     uint32_t apos = 0xFFFFFFFFu;
     const uint32_t cap = max_steps < Q + L ? max_steps : Q + L;
@@ -157,13 +160,15 @@ __device__ __forceinline__ SysOut fpp_sysd_group(uint64_t q, uint64_t &touched, 
     // after tau steps position p is at lane (tau - 1 - p) & 63
     const uint32_t src = (tau - 1u - pos) & 63u;
     const uint32_t ncf = sys_pull(src, xc), nmf = sys_pull(src, xm), ncu = sys_pull(src, xu);
-    if (live) { rcf = ncf; rmf = nmf; rcu = ncu; }
+    rcf = live ? ncf : rcf;
+    rmf = live ? nmf : rmf;
+    rcu = live ? ncu : rcu;
     const uint32_t nl = lfull ? (apos & 63u) : sys_pull(apos & 63u, pmap);
     const uint32_t cnode = apos != 0xFFFFFFFFu ? gbg + nl : 0xFFFFFFFFu;
     const uint32_t back = qpre ? cnode : sys_pull(rq, cnode);
     const uint32_t open = k < L ? 1u : 0u;
     const uint32_t open_here = qpre ? open : sys_pull(rq, open);
-    if (inq) asg = back;
+    asg = inq ? back : asg;
     out.left = __builtin_amdgcn_ballot_w64(inq && open_here != 0);
     if (TOUCHED) {
         const uint32_t bl = apos != 0xFFFFFFFFu && nl < 32 ? 1u << nl : 0u;
