@@ -266,12 +266,9 @@ using RecT = uint32_t[G];
 constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
 // the systolic group fill (fp_pipe_sys.h) is compiled for stages of at most this many groups
 constexpr uint32_t SYS_MAX_G = 4;
-// ... and for the multi-stage 1024-thread kernels of up to this many groups (k_ffd_pipe<10, 1024>: 128
-// VGPRs with 7 spilled; <16, 1024> would spill 75)
-constexpr uint32_t SYS_MAX_G_1024 = 10;
 // The serial loop over one group's queue is the exec-masked loop (fp_pipe_asm.h fpp_group_x:
 // 172 vs 264 cycles per container for round 2's readlane / writelane loop).
-template <uint32_t G, bool UPD, bool SYS, uint32_t... gs, class Rec>
+template <uint32_t G, bool UPD, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
@@ -309,7 +306,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                 const unsigned long long gc0 = STAT_GCLK();
                 // long queues (a filling group): the systolic loop, else the serial one
                 // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
-                if (SYS && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
+                if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
                     fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                          req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm, sys >> 16);
                 else
@@ -386,10 +383,6 @@ k_ffd_pipe(const PipeArgs a_arg) {
     const uint32_t pmask = a.kpack ? IDX_POS_MASK : ~CYC;
     // per-lane group bit sets (schedulable / candidate groups): 64-bit above 32 groups
     using GM = typename std::conditional<(G > 32), uint64_t, uint32_t>::type;
-    // the systolic fill is compiled for the narrow stages and the multi-stage 1024-thread kernels
-    // (a 128-VGPR budget); the one-wave wide kernels (BLK 64) keep their register budget for the
-    // waves per SIMD the throughput regime needs
-    constexpr bool SYS_OK = G <= SYS_MAX_G || (BLK == 1024 && G <= SYS_MAX_G_1024);
 
     uint64_t *M = reinterpret_cast<uint64_t *>(smem);
     uint32_t *CTL = reinterpret_cast<uint32_t *>(M + (size_t)W * G * K * 2);
@@ -714,7 +707,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
             if (prio == 1u && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
             if (todo)
-                fpp_groups<G, (G > 1), SYS_OK>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+                fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
                                        __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
@@ -1476,8 +1469,7 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     // Default: queues of >= 32 containers in the narrow stages (configs 2 / 3 / 5: one scenario,
     // one-group stages); config 3's k_ffd_pipe 72.1 -> 65.2 ms, config 2 0.81 -> 0.75 ms, every
     // threshold from 1 to 48 within 1 % (tools/sys_sweep.py, profiles/r03c_sys_sweep.jsonl)
-    g->sys = G <= SYS_MAX_G || (!wide_g(W, G) && G <= SYS_MAX_G_1024)
-                 ? (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, G <= SYS_MAX_G ? 32 : 0) : 0u;
+    g->sys = G <= SYS_MAX_G ? (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 32) : 0u;
     if (g->sys > 64) g->sys = 64;
     g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
     if (g->sys_extra > 128) g->sys_extra = 128;

@@ -120,12 +120,11 @@ def test_geometry_query_defaults(planner):
 def test_systolic_fill_vs_oracle(C, N, flags, w, seg, thr, valu, planner, O, opts):
     """Group queues of >= thr containers take the systolic loop (thr 1: every queue), the rest
     the serial one; the plan, reasons and final node state must be the oracle's.  The systolic
-    loop is compiled for stages of at most 4 groups and for the 1024-thread kernels of at most 10
-    (fp_pipe.hip SYS_MAX_G, SYS_MAX_G_1024): wider stages report 0 and run the serial loop."""
+    loop is compiled for stages of at most 4 groups (FP_SYS_MAX_G): wider stages report 0 and
+    run the serial loop on the same inputs."""
     opts(systolic=thr, pipe_w=w, pipe_seg=seg, systolic_valu=valu)
     g = planner.geometry(1, C, N)
-    # compiled for stages of <= 4 groups and the 1024-thread kernels of <= 10 (fp_pipe.hip SYS_MAX_G*)
-    assert g["systolic"] == (thr if g["groups"] <= 10 else 0), g
+    assert g["systolic"] == (thr if g["groups"] <= 4 else 0), g
     cont, nodes = O.gen_scenario(SEED4 + 23 * C + N, 2, C, N, flags)
     assign, reason, after = planner.place(cont, nodes)
     ea, er, eafter, _ = O.place(cont, nodes)
