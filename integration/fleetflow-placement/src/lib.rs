@@ -105,6 +105,71 @@ impl Planner {
         })?;
         Ok((assign, reason))
     }
+
+    /// One stage's whole dry-run plan in one call (fleetplace.h `fp_plan_stage`, the
+    /// `fleet up --dry-run` path of up.rs:57-136): the legacy order, the Kahn levels and start
+    /// order and, with `placement = Some((containers, nodes))` (container v = vertex v), the
+    /// stage-2 first feasible server and count per service and the FFD plan, `nodes` updated
+    /// in place.  A stage of <= 512 services is one kernel launch.
+    pub fn plan_stage(&mut self, row_ptr: &[u32], col: &[u32], has_deps: &[u8],
+                      placement: Option<(&Containers, &mut Nodes)>) -> Result<StagePlan, PlanError> {
+        let v = has_deps.len();
+        if v > 0 && row_ptr.len() != v + 1 {
+            return Err(PlanError(ffi::FP_EINVAL));
+        }
+        let g = ffi::fp_graph { n_vertices: v as u32, n_edges: col.len() as u32, row_ptr: row_ptr.as_ptr(),
+                                col: if col.is_empty() { std::ptr::null() } else { col.as_ptr() },
+                                has_deps: has_deps.as_ptr() };
+        let mut out = StagePlan { perm: vec![0; v], level: vec![0; v], order: vec![0; v], n_cycle: 0,
+                                  first: vec![], count: vec![], assign: vec![], reason: vec![] };
+        let rc = match placement {
+            None => unsafe {
+                ffi::fp_plan_stage(self.ctx, &g, std::ptr::null(), std::ptr::null_mut(), out.perm.as_mut_ptr(),
+                                   out.level.as_mut_ptr(), out.order.as_mut_ptr(), &mut out.n_cycle,
+                                   std::ptr::null_mut(), std::ptr::null_mut(), std::ptr::null_mut(),
+                                   std::ptr::null_mut())
+            },
+            Some((c, nodes)) => {
+                if !c.all_len(v) || !nodes.all_len(nodes.cpu_free.len()) {
+                    return Err(PlanError(ffi::FP_EINVAL));
+                }
+                let cs = ffi::fp_containers { n: v as u32, cpu_m: c.cpu_m.as_ptr(), mem_mib: c.mem_mib.as_ptr(),
+                                              req_labels: c.req_labels.as_ptr(), conflict: c.conflict.as_ptr() };
+                let mut ns = ffi::fp_nodes { n: nodes.cpu_free.len() as u32, cpu_free: nodes.cpu_free.as_mut_ptr(),
+                                             mem_free: nodes.mem_free.as_mut_ptr(), labels: nodes.labels.as_ptr(),
+                                             conflict_used: nodes.conflict_used.as_mut_ptr(),
+                                             schedulable: nodes.schedulable.as_ptr() };
+                out.first = vec![0; v];
+                out.count = vec![0; v];
+                out.assign = vec![0; v];
+                out.reason = vec![0; v];
+                unsafe {
+                    ffi::fp_plan_stage(self.ctx, &g, &cs, &mut ns, out.perm.as_mut_ptr(), out.level.as_mut_ptr(),
+                                       out.order.as_mut_ptr(), &mut out.n_cycle, out.first.as_mut_ptr(),
+                                       out.count.as_mut_ptr(), out.assign.as_mut_ptr(), out.reason.as_mut_ptr())
+                }
+            }
+        };
+        check(rc)?;
+        Ok(out)
+    }
+}
+
+/// The result of [`Planner::plan_stage`], per vertex of the stage graph.  The placement
+/// vectors are empty for a stage planned without servers.
+pub struct StagePlan {
+    /// A1 legacy start order (engine.rs:64-85)
+    pub perm: Vec<u32>,
+    /// A2 start level (FP_NONE = CYCLE) and the (level, index) start order
+    pub level: Vec<u32>,
+    pub order: Vec<u32>,
+    pub n_cycle: u32,
+    /// stage 2 on the pristine server table: first feasible server (FP_NONE) and count
+    pub first: Vec<u32>,
+    pub count: Vec<u32>,
+    /// A6 FFD: server per service (FP_NONE if unplaced) and reason (FP_REASON_*)
+    pub assign: Vec<u32>,
+    pub reason: Vec<u8>,
 }
 
 impl Planner {
@@ -386,6 +451,33 @@ pub fn place_stage(flow: &Flow, stage_name: &str, c: &Containers, nodes: &mut No
     }
     let (assign, _) = with_planner(|p| p.place(c, nodes, None))?;
     Ok(assign.iter().map(|&a| if a == ffi::FP_NONE { None } else { Some(stage.servers[a as usize].clone()) }).collect())
+}
+
+/// What `fleet up --dry-run` prints for a stage (up.rs:57-136), planned in one call: the
+/// reference's start order, the start level of every service (`None` = CYCLE) and, when the
+/// stage has servers and `placement` carries their tables, each service's server.  A stage
+/// whose service list repeats a name is planned per vertex (first occurrence) and mapped back.
+pub fn dry_run_stage(services: &[String], flow: &Flow, placement: Option<(&Containers, &mut Nodes)>)
+                     -> Result<(Vec<String>, Vec<Option<u32>>, Option<Vec<Option<u32>>>), PlanError> {
+    if services.is_empty() {
+        return Ok((Vec::new(), Vec::new(), placement.map(|_| Vec::new())));
+    }
+    let (pos, row_ptr, col, has_deps) = stage_graph(services, flow);
+    let placed = placement.is_some();
+    let plan = with_planner(|p| p.plan_stage(&row_ptr, &col, &has_deps, placement))?;
+    // the legacy order runs over positions (engine.rs:64-85 keeps duplicates); without
+    // duplicates positions and vertices coincide
+    let order = if pos.len() == has_deps.len() {
+        plan.perm.iter().map(|&i| services[i as usize].clone()).collect()
+    } else {
+        try_order_by_dependencies(services, flow)?
+    };
+    let levels = pos.iter().map(|&v| match plan.level[v as usize] { ffi::FP_NONE => None, l => Some(l) }).collect();
+    let servers = placed.then(|| pos.iter().map(|&v| match plan.assign[v as usize] {
+        ffi::FP_NONE => None,
+        a => Some(a),
+    }).collect());
+    Ok((order, levels, servers))
 }
 
 #[cfg(all(test, feature = "gpu-tests"))]
