@@ -188,6 +188,11 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t my_t, int bas
     return k;
 }
 
+// number of set bits of a wave mask below this lane (v_mbcnt: no per-lane below-mask kept live)
+__device__ __forceinline__ uint32_t fpp_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // min over the wave's 64 lanes, broadcast (DPP row shifts + row broadcasts into lane 63;
 // lanes without a DPP source read UINT32_MAX, the identity of min)
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
@@ -264,23 +269,27 @@ using RecT = uint32_t[G];
 // (<= 4-group) stages 4 -- config 3 65.3 -> 64.1 ms (16: 65.3, 32: 70.8); wide stages off -- config
 // 4 17.54 -> 17.28 ms (4: 17.48, 32: 17.96).
 constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
+// lane selects by inverse ballot in the one-wave kernels' group bookkeeping (fpp_lane_sel)
+#ifndef FPP_IB
+#define FPP_IB 1
+#endif
 // the systolic group fill (fp_pipe_sys.h) is compiled for stages of at most this many groups
 constexpr uint32_t SYS_MAX_G = 4;
 // The serial loop over one group's queue is the exec-masked loop (fp_pipe_asm.h fpp_group_x:
 // 172 vs 264 cycles per container for round 2's readlane / writelane loop).
-template <uint32_t G, bool UPD, uint32_t... gs, class Rec>
+template <uint32_t G, bool UPD, bool IB, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
-                                           uint64_t *Mw, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
+                                           uint64_t *Mw, uint32_t mlane, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
                                            uint32_t &nhit, uint32_t sys, unsigned long long (&gst)[4]) {
     constexpr uint32_t pf_max = G <= SYS_MAX_G ? PF_MAX_NARROW : PF_MAX_WIDE;
     (
         [&] {
             uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
             if (pf_max > 0 && q) {
-                uint64_t e = __builtin_amdgcn_ballot_w64((rcf[gs] >= qc) & (rmf[gs] >= qm));
+                uint64_t e = (__builtin_amdgcn_ballot_w64(rcf[gs] >= qc) & __builtin_amdgcn_ballot_w64(rmf[gs] >= qm));
                 if (__builtin_popcountll(e) <= pf_max) {
                     bool ok = false;
                     while (e) {
@@ -310,29 +319,59 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                     fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                          req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm, sys >> 16);
                 else
-                    fpp_group_x<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                    fpp_group_x<gs, G, IB>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
                                        req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
                 const unsigned long long gc1 = STAT_GCLK();
                 if (STAT_FINE) { gst[0] += gc1 - gc0; gst[2] += 1; gst[3] += (uint32_t)__builtin_popcountll(touched); }
                 if (touched) {
-                    const bool me = (touched >> lane) & 1ull;
-                    if (gs < 32) used |= me ? (1u << gs) : 0u;
-                    else used_hi |= me ? (1u << (gs & 31)) : 0u;
-                    if (UPD) {
-                        uint64_t clr = 0, tt = touched;
-                        while (tt) {
-                            const uint32_t l = (uint32_t)__builtin_ctzll(tt);
-                            tt &= tt - 1;
-                            const uint32_t nc = __builtin_amdgcn_readlane(rcf[gs], l);
-                            const uint32_t nm = __builtin_amdgcn_readlane(rmf[gs], l);
-                            // a bit at or below the node's new free capacity stays; every bit above
-                            // it goes (clearing a bit that was already clear is harmless, so the
-                            // capacity before the queue is not needed)
-                            clr |= (my_t > (lane < 32 ? nc : nm)) ? (1ull << l) : 0ull;
+                    if constexpr (IB) {
+                        // one-wave kernels: lane selects read the masks directly (fpp_lane_sel).
+                        // Bucket lane k clears node l's bit when the node's new free capacity is
+                        // below T[k] (cpu for lanes 0-31, mem for 32-63): per touched node, two
+                        // compares give the lanes to clear as a wave mask, and one select per half
+                        // sets bit l there.
+                        if (gs < 32) used = fpp_lane_sel<true>(touched, used | (1u << gs), used);
+                        else used_hi = fpp_lane_sel<true>(touched, used_hi | (1u << (gs & 31)), used_hi);
+                        if (UPD) {
+                            uint32_t clr_lo = 0, clr_hi = 0;
+                            uint64_t tt = touched;
+                            while (tt) {
+                                const uint32_t l = (uint32_t)__builtin_ctzll(tt);
+                                tt &= tt - 1;
+                                const uint32_t nc = __builtin_amdgcn_readlane(rcf[gs], l);
+                                const uint32_t nm = __builtin_amdgcn_readlane(rmf[gs], l);
+                                const uint64_t below = (__builtin_amdgcn_ballot_w64(my_t > nc) & 0xFFFFFFFFull) |
+                                                       (__builtin_amdgcn_ballot_w64(my_t > nm) & ~0xFFFFFFFFull);
+                                if (l < 32) clr_lo = fpp_lane_sel<true>(below, clr_lo | (1u << l), clr_lo);
+                                else clr_hi = fpp_lane_sel<true>(below, clr_hi | (1u << (l & 31)), clr_hi);
+                            }
+                            const uint64_t clr = ((uint64_t)clr_hi << 32) | clr_lo;
+                            // the group's mask word of this bucket lane at an immediate offset from one
+                            // per-lane LDS address (a per-group address was hoisted and spilled)
+                            if (__builtin_amdgcn_ballot_w64(clr != 0))
+                                asm volatile("ds_and_b64 %0, %1 offset:%2" ::"v"(mlane), "v"(~clr),
+                                             "i"(gs * K * 2 * 8) : "memory");
                         }
-                        if (__builtin_amdgcn_ballot_w64(clr != 0))
-                            atomicAnd((unsigned long long *)&Mw[(size_t)gs * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
-                                      ~clr);
+                    } else {
+                        const bool me = (touched >> lane) & 1ull;
+                        if (gs < 32) used |= me ? (1u << gs) : 0u;
+                        else used_hi |= me ? (1u << (gs & 31)) : 0u;
+                        if (UPD) {
+                            uint64_t clr = 0, tt = touched;
+                            while (tt) {
+                                const uint32_t l = (uint32_t)__builtin_ctzll(tt);
+                                tt &= tt - 1;
+                                const uint32_t nc = __builtin_amdgcn_readlane(rcf[gs], l);
+                                const uint32_t nm = __builtin_amdgcn_readlane(rmf[gs], l);
+                                // a bit at or below the node's new free capacity stays; every bit above
+                                // it goes (clearing a bit that was already clear is harmless, so the
+                                // capacity before the queue is not needed)
+                                clr |= (my_t > (lane < 32 ? nc : nm)) ? (1ull << l) : 0ull;
+                            }
+                            if (__builtin_amdgcn_ballot_w64(clr != 0))
+                                atomicAnd((unsigned long long *)&Mw[(size_t)gs * K * 2 + (lane & (K - 1)) * 2 + (lane >> 5)],
+                                          ~clr);
+                        }
                     }
                 }
                 if (STAT_FINE) gst[1] += STAT_GCLK() - gc1;
@@ -375,8 +414,14 @@ k_ffd_pipe(const PipeArgs a_arg) {
     const PipeArgs &a = a_arg;  // the host pass only type-checks the body
 #endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t W = a.W, R = a.R, B = a.B, prio = a.prio;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // one-wave segments (BLK == 64) are a compile-time W = 1: the LDS-ring paths between stages
+    // of a segment drop out of those kernels
+#ifndef FPP_W1
+#define FPP_W1 1
+#endif
+    constexpr bool one_wave = BLK == 64 && FPP_W1;
+    const uint32_t W = one_wave ? 1u : a.W, R = a.R, B = a.B, prio = a.prio;
+    const uint32_t w = one_wave ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t C = a.C, N = a.N;
     // the FFD position inside an s_idx word (above it: CYCLE bit 31, packed buckets)
@@ -425,6 +470,8 @@ k_ffd_pipe(const PipeArgs a_arg) {
     const uint32_t my_t = a.thr[lane];
     const uint32_t gbase = (b * W + w) * G;             // first (global) group of this tile
     uint64_t *Mw = M + (size_t)w * G * K * 2;           // the tile's masks
+    // LDS byte address of this bucket lane's mask word of group 0 (one-wave kernels' mask upkeep)
+    const uint32_t mlane = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t *)(Mw + (lane & (K - 1)) * 2 + (lane >> 5));
     // The tile's node records.  Unschedulable (and padding) nodes are stored so that every
     // container with a nonzero field fails the exact check on them: cpu = mem = 0, all
     // conflict bits used, all (inverted) label bits missing.  The all-zero container, which
@@ -662,7 +709,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
         GM cand = 0;
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
-            const uint64_t e = __builtin_amdgcn_ballot_w64((rcf[g] >= qc) & (rmf[g] >= qm));
+            const uint64_t e = (__builtin_amdgcn_ballot_w64(rcf[g] >= qc) & __builtin_amdgcn_ballot_w64(rmf[g] >= qm));
             const uint64_t *mg = Mw + (size_t)g * K * 2;
             if (prescan_skip) {
                 // a group whose corner is empty fits no container of the batch: no mask loads
@@ -707,9 +754,9 @@ k_ffd_pipe(const PipeArgs a_arg) {
             unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
             if (prio == 1u && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
             if (todo)
-                fpp_groups<G, (G > 1)>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+                fpp_groups<G, (G > 1), BLK == 64 && FPP_IB>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
-                                       (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw,
+                                       (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw, mlane,
                                        __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
             if (prio == 1u && todo) __builtin_amdgcn_s_setprio(0);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
@@ -755,7 +802,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             const uint64_t fm = __builtin_amdgcn_ballot_w64(fwd);
             const uint32_t f = (uint32_t)__popcll(fm);
             if (f) {
-                const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+                const uint32_t pos = ofill + fpp_rank(fm);
                 // slots ohead and ohead + 1 must be free (wave-uniform; bounded links only)
                 if (gbounded &&
                     !gring_wait(gout_head + LCTL / 2, ohead + 2, gslots, otail_seen, a, abort_flag, lane, st_spin_out)) {
@@ -802,7 +849,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
         const uint64_t fm = __ballot(fwd);
         const uint32_t f = (uint32_t)__popcll(fm);
         if (f) {
-            const uint32_t pos = ofill + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+            const uint32_t pos = ofill + fpp_rank(fm);
             uint32_t *od = odata + (size_t)(ohead % R) * NF * 64;
             if (fwd && pos < 64) {
                 od[pos] = cpu; od[64 + pos] = mem; od[128 + pos] = req; od[192 + pos] = conf; od[256 + pos] = idx;

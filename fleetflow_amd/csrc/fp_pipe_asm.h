@@ -18,6 +18,19 @@ __device__ __forceinline__ uint64_t fpp_uniform64(uint64_t x) {
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
 }
 
+// Per-lane select by a wave-uniform lane mask: lane i gets `set` when bit i of m is set, else
+// `clr`.  IB: one v_cndmask reading the mask as its condition register pair (inverse ballot)
+// instead of the 64-bit shift, and and compare of the C++ form.  Only the one-wave kernels use it:
+// in the 1024-thread kernels the compiler holds some of these masks in VGPRs, which the inverse
+// ballot cannot read ("illegal VGPR to SGPR copy").
+template <bool IB>
+__device__ __forceinline__ uint32_t fpp_lane_sel(uint64_t m, uint32_t set, uint32_t clr) {
+    if constexpr (IB)
+        return __builtin_amdgcn_inverse_ballot_w64(m) ? set : clr;
+    else
+        return ((m >> __lane_id()) & 1ull) ? set : clr;
+}
+
 #ifdef FP_PIPE_STATS
 #define FPP_ASM_CNT_CHECK "s_add_u32 %[nchk], %[nchk], 1\n\t"
 #else
@@ -117,7 +130,7 @@ __device__ __forceinline__ void fpp_refilter_loop(uint64_t q, uint64_t &touched,
     // nothing, finishes the queue in the plain loop.
     fpp_asm_group_x<true>(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gbg, nchk);
     while (q) {
-        uint64_t e = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
+        uint64_t e = (__builtin_amdgcn_ballot_w64(rcf >= qc) & __builtin_amdgcn_ballot_w64(rmf >= qm));
         uint64_t fit = 0;
         if (__builtin_popcountll(e) <= REFILTER_MAX) {
             bool ok = false;
@@ -143,7 +156,7 @@ __device__ __forceinline__ void fpp_refilter_loop(uint64_t q, uint64_t &touched,
 
 // The serial group loop (fpp_groups): the exec-masked loop with its re-test plus the per-group
 // vector epilogue -- placed bits of the hits, next candidate group of the misses.
-template <uint32_t g, uint32_t G>
+template <uint32_t g, uint32_t G, bool IB = false>
 __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64_t &touched, uint32_t &asg,
                                             uint32_t &nxt, uint32_t &rcf, uint32_t &rmf, uint32_t &rcu,
                                             uint32_t rlab, uint32_t cpu, uint32_t mem, uint32_t req, uint32_t conf,
@@ -152,9 +165,13 @@ __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64
     const uint64_t q0 = q;
     fpp_refilter_loop(q, touched, asg, rcf, rmf, rcu, rlab, cpu, mem, req, conf, gb64 + g * 64u, nchk, qc, qm);
     q = q0;
-    const uint32_t lane = __lane_id();
-    const bool inq = (q >> lane) & 1ull;
-    const uint64_t hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);
+    uint64_t hit;
+    if constexpr (IB) {  // one-wave kernels: q is a wave-uniform SGPR mask
+        hit = q & __builtin_amdgcn_ballot_w64(asg != 0xFFFFFFFFu);
+    } else {
+        const bool inq = (q >> __lane_id()) & 1ull;
+        hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);
+    }
 #ifdef FP_PIPE_STATS
     nhit += (uint32_t)__builtin_popcountll(hit);
 #else
@@ -164,7 +181,8 @@ __device__ __forceinline__ void fpp_group_x(uint64_t q, uint64_t &placed, uint64
     {  // the misses move on to their next candidate group (a select: no divergent branch)
         const uint64_t above = (((uint64_t)cand_hi << 32) | cand) & ~((2ull << g) - 1ull);
         const uint32_t nx = above ? (uint32_t)__builtin_ctzll(above) : G;
-        nxt = (inq && asg == 0xFFFFFFFFu) ? nx : nxt;
+        if constexpr (IB) nxt = fpp_lane_sel<true>(q & ~hit, nx, nxt);
+        else nxt = (((q >> __lane_id()) & 1ull) && asg == 0xFFFFFFFFu) ? nx : nxt;
     }
 }
 

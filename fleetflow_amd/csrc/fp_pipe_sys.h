@@ -150,7 +150,7 @@ __device__ __forceinline__ SysOut fpp_sys_group(uint64_t q, uint64_t &touched, u
     SysOut out{0};
     // live nodes: the batch corner (a node outside it fits no container of the batch, now or
     // later) -> positions 0..L-1, in node order
-    const uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
+    const uint64_t lm = (__builtin_amdgcn_ballot_w64(rcf >= qc) & __builtin_amdgcn_ballot_w64(rmf >= qm));
     const uint32_t L = (uint32_t)__builtin_popcountll(lm);
     if (L == 0) {  // nothing can fit: every queued container misses the group
         if ((q >> lane) & 1ull) asg = 0xFFFFFFFFu;

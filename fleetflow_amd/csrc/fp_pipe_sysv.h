@@ -97,7 +97,7 @@ __device__ __forceinline__ SysOut fpp_sysv_group(uint64_t q, uint64_t &touched, 
     const uint32_t lane = __lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     SysOut out{0};
-    const uint64_t lm = __builtin_amdgcn_ballot_w64((rcf >= qc) & (rmf >= qm));
+    const uint64_t lm = (__builtin_amdgcn_ballot_w64(rcf >= qc) & __builtin_amdgcn_ballot_w64(rmf >= qm));
     const uint32_t L = (uint32_t)__builtin_popcountll(lm);
     if (L == 0) {
         if ((q >> lane) & 1ull) asg = 0xFFFFFFFFu;

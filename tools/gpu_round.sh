@@ -2,7 +2,7 @@
 # One GPU session: error-path tests (isolated, short limit), the -m gpu suite, the bench
 # (config 4 at 4096 + config 3 leg + CPU baseline), then the rocprofv3 passes.
 # Usage: tools/gpu_round.sh <tag> [steps...]
-#   steps: errors tests bench scale prof kt lvl sortstats pipestats model front ab (default: errors tests bench prof)
+#   steps: errors tests bench scale prof kt lvl sortstats pipestats model front ab sq sweep (default: errors tests bench prof)
 #   kt = config-4 kernel trace (tools/ktrace.sh), lvl = config-5 levelizer timing + kernel stats
 #   (tools/gpu_lvl.sh), sortstats / pipestats / model = diagnostics-build runs (k_scen_sort phases,
 #   per-stage pipeline counters at 4096 scenarios, the latency model of tools/pipe_model.py)
@@ -68,6 +68,14 @@ for s in $steps; do
       tools/ab_variants.sh $tag "${AB_LIBS:--}" ${AB_LOADS:-c4x4096,c3} > ${log}_ab.txt 2>&1 \
         || { echo "ab failed"; tail -20 ${log}_ab.txt; exit 1; }
       cat ${log}_ab.txt ;;
+    sq)
+      # SQ instruction / wave counters of the config-4 kernel for each library build: SQ_LIBS="- _suffix ..."
+      for v in ${SQ_LIBS:--}; do
+        [ "$v" = "-" ] && v=""
+        FLEETPLACE_LIB=$root/fleetflow_amd/libfleetplace$v.so SQ_PASSES=${SQ_PASSES:-1} bash tools/pmc_sq.sh ${tag}$v \
+          || { echo "sq $v failed"; exit 1; }
+        python tools/sq_summary.py ${tag}$v k_ffd_pipe
+      done ;;
     sweep)
       # one context option over device-resident loads: SWEEP_OPT, SWEEP_VALUES, SWEEP_LOADS (tools/sys_sweep.py)
       timeout -k 10 400 python -u tools/sys_sweep.py --opt ${SWEEP_OPT:?} --values=${SWEEP_VALUES:?} \

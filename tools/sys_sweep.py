@@ -17,11 +17,13 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 from fleetflow_amd import DevBatch, Planner  # noqa: E402
-from fleetflow_amd._lib import FP_K_PLACE  # noqa: E402
+from fleetflow_amd._lib import FP_K_PLACE, FP_K_SORT  # noqa: E402
 
 LOADS = {"c3": (1, 1_000_000, 100_000, 0x5EED0003), "c2": (1, 10_000, 1_000, 0x5EED0002),
          "c4x512": (512, 50_000, 5_000, 0x5EED0004), "c4x1024": (1024, 50_000, 5_000, 0x5EED0004),
-         "c4x2048": (2048, 50_000, 5_000, 0x5EED0004), "c4x4096": (4096, 50_000, 5_000, 0x5EED0004)}
+         "c4x2048": (2048, 50_000, 5_000, 0x5EED0004), "c4x4096": (4096, 50_000, 5_000, 0x5EED0004),
+         # many small scenarios (the LDS sort's one-workgroup-per-scenario sizing)
+         "s4096c6000": (4096, 6_000, 600, 0x5EED0006)}
 
 
 def main():
@@ -46,7 +48,7 @@ def main():
             ref = None
             for v in [int(x) for x in args.values.split(",")]:
                 p.set_option(args.opt, v)
-                times, walls = [], []
+                times, walls, sorts = [], [], []
                 for r in range(args.reps + 1):
                     db.restore_nodes(snap)
                     torch.cuda.synchronize()
@@ -56,9 +58,11 @@ def main():
                     p.sync()
                     w = time.perf_counter() - t0
                     ms, n = p.kernel_stats(FP_K_PLACE)
+                    sms, sn = p.kernel_stats(FP_K_SORT)
                     p.profile(False)
                     if r:
                         times.append(ms / max(n, 1))
+                        sorts.append(sms / max(sn, 1))
                         walls.append(w * 1e3)
                 same = None
                 if ref is None:
@@ -71,6 +75,7 @@ def main():
                 del wts
                 print(json.dumps({"load": load, "S": S, "C": C, "N": N, "opt": args.opt, "value": v, "digest": digest,
                                   "ffd_ms": round(statistics.median(times), 3),
+                                  "sort_ms": round(statistics.median(sorts), 3),
                                   "wall_ms": round(statistics.median(walls), 3), "same_plan": same,
                                   "geometry": p.geometry(S, C, N)}), flush=True)
             p.set_option(args.opt)
