@@ -273,6 +273,9 @@ constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
 #ifndef FPP_IB
 #define FPP_IB 1
 #endif
+#ifndef FPP_IB1024  // ... and in the 1024-thread kernels of more than SYS_MAX_G groups: off, slower there
+#define FPP_IB1024 0  // (512 / 1024 scenarios 6.43 / 7.79 vs 6.21 / 7.58 ms, profiles/r05n_ib1024_ab.jsonl)
+#endif
 // the systolic group fill (fp_pipe_sys.h) is compiled for stages of at most this many groups
 constexpr uint32_t SYS_MAX_G = 4;
 // The serial loop over one group's queue is the exec-masked loop (fp_pipe_asm.h fpp_group_x:
@@ -394,7 +397,13 @@ constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
 // more than the extra slots buy (profiles/r04x_waves_ab.jsonl).  The 8-group segments of batches of up to
 // 1024 scenarios stay at five waves (k_ffd_pipe<8, 1024>, 82 VGPRs): six or seven waves ran 1024
 // scenarios 8.69 / 9.18 vs 8.46-8.54 ms (profiles/r04ab_small8_waves_ab.jsonl)
-constexpr uint32_t WIDE12_BIG_WAVES = 6, WIDE12_BIG_S = 4096;
+#ifndef FPP_BIG_WAVES
+#define FPP_BIG_WAVES 6
+#endif
+#ifndef FPP_BIG_S
+#define FPP_BIG_S 4096
+#endif
+constexpr uint32_t WIDE12_BIG_WAVES = FPP_BIG_WAVES, WIDE12_BIG_S = FPP_BIG_S;
 // Batch prescan: a group with an empty batch corner skips its bucket-mask loads in the wide stages
 // (config-4 FFD 17.38 -> 15.72 ms: a batch that passes a segment mostly has every corner empty);
 // the narrow stages keep the branch-free form (config 3: 64.3 vs 65.3 ms with the skip; r03z A/B,
@@ -754,7 +763,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
             if (prio == 1u && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
             if (todo)
-                fpp_groups<G, (G > 1), BLK == 64 && FPP_IB>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+                fpp_groups<G, (G > 1), (BLK == 64 || (FPP_IB1024 && G > SYS_MAX_G)) && FPP_IB>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw, mlane,
                                        __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
