@@ -107,6 +107,8 @@ struct PipeArgs {
     uint32_t flush;   // idle flushes of partial output slots: bit 0 LDS rings, bit 1 global links (bounded)
     uint32_t kpack;   // 1: s_idx carries the bucket indices (bits 21-25 cpu, 26-30 mem; C <= 2^21)
     uint32_t publish; // full slots per head publish on a global link (1 when bounded: see the kernel)
+    uint32_t pub_mask; // the unbounded-only kernel publishes when (head & pub_mask) == 0 (a power of two
+                       // <= publish, minus 1): no loop-carried counter
     uint32_t sys;     // systolic group fill: queues of >= (sys & 0xFFFF) containers, (sys >> 16) extra
                       // steps before the serial finish (0: serial loop only)
     uint32_t *ticket; // workgroup ticket -> (scenario, segment) in launch order
@@ -128,8 +130,12 @@ struct PipeArgs {
     uint32_t prio;          // wave priority mode (FP_PRIO_LEVEL comment)
 };
 
+// Control words (heads, tails, counts, abort flags) are read by every lane at one address: the
+// loads below return them wave-uniform (readfirstlane), so that the loop exits they decide are
+// uniform too.  Divergence analysis cannot see that a same-address load is uniform; a loop exit it
+// believes divergent keeps every loop-carried counter of the kernel in VGPRs (and spills them).
 __device__ __forceinline__ uint32_t lds_acq(uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 __device__ __forceinline__ void lds_rel(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -142,6 +148,9 @@ __device__ __forceinline__ void lds_rel(uint32_t *p, uint32_t v) {
 // dword with sc1 loads, so no acquire fence is needed.
 __device__ __forceinline__ uint32_t g_ld(const uint32_t *p) {
     return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t g_ld_u(const uint32_t *p) {  // a control word: wave-uniform
+    return __builtin_amdgcn_readfirstlane(g_ld(p));
 }
 __device__ __forceinline__ void g_st(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -218,9 +227,9 @@ __device__ __forceinline__ bool gring_wait(uint32_t *tail, uint32_t need, uint32
     uint32_t n = 0;
     uint64_t t0 = 0;
     while (true) {
-        seen = __builtin_amdgcn_readfirstlane(g_ld(tail));
+        seen = g_ld_u(tail);
         if (need - seen <= slots) { iters += n; return true; }
-        if (g_ld(a.gabort) || lds_acq(abort_flag)) return false;
+        if (g_ld_u(a.gabort) || lds_acq(abort_flag)) return false;
         if ((++n & 255u) == 0) {
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
             if (!t0) {
@@ -550,7 +559,13 @@ k_ffd_pipe(const PipeArgs a_arg) {
     // bounded links: the consumer publishes how many slots it has finished with (tail, a
     // separate 128-B line); the producer writes slot h only while h - tail < slots.  Slot
     // index = sequence number mod slots (identity when unbounded: slots >= every slot).
-    const uint32_t gslots = a.slots, gbounded = a.bounded;
+    // the six-wave many-scenario kernel only ever runs unbounded links (lag = S phases; the launch
+    // takes the five-wave one when a bounded ring is forced): slot index = sequence number, and the
+    // ring waits, tail publishes and idle flushes of the global links compile out
+    constexpr bool unbounded_only = BLK == 64 && WV != 0;
+    const uint32_t gslots = a.slots, gbounded = unbounded_only ? 0u : a.bounded;
+    const uint32_t gflush = unbounded_only ? (a.flush & 1u) : a.flush;
+#define GSLOT(i) (unbounded_only ? (uint32_t)(i) : (uint32_t)(i) % gslots)
     uint32_t otail_seen = 0;                            // last tail read from the consumer
     uint32_t *octl = CTL + w * 8;
     uint32_t *ictl = CTL + (w - 1) * 8;
@@ -589,9 +604,9 @@ k_ffd_pipe(const PipeArgs a_arg) {
             uint64_t t0 = 0;
             bool got = itail < ihead_seen;  // a head seen earlier already covers this slot: no poll
             while (!got) {
-                ihead_seen = __builtin_amdgcn_readfirstlane(g_ld(gin_head));
+                ihead_seen = g_ld_u(gin_head);
                 if (ihead_seen > itail) { got = true; break; }
-                if (g_ld(a.gabort) || lds_acq(abort_flag)) break;
+                if (g_ld_u(a.gabort) || lds_acq(abort_flag)) break;
                 if ((++n_sp & 255u) == 0) {
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     if (!t0) {
@@ -617,9 +632,11 @@ k_ffd_pipe(const PipeArgs a_arg) {
             // reuse them.  Published every 4 slots (the ring keeps that much slack).
             // With idle flushes the producer reads it as "the consumer is on my last slot":
             // published every slot then.
-            if (((a.flush & 2u) || (gbounded && (itail & 3u) == 0)) && lane == 0) g_st(gin_head + LCTL / 2, itail);
-            const uint32_t *sd = gin_data + (size_t)(itail % gslots) * LSLOT;
-            const uint32_t n = g_ld(sd);
+            if (((gflush & 2u) || (gbounded && (itail & 3u) == 0)) && lane == 0) g_st(gin_head + LCTL / 2, itail);
+            const uint32_t *sd = gin_data + (size_t)GSLOT(itail) * LSLOT;
+            // the count is wave-uniform: say so, or the loop exit below reads as divergent and every
+            // loop-carried counter of the kernel is kept (and spilled) in VGPRs
+            const uint32_t n = g_ld_u(sd);
             const uint32_t pos = g_ld(sd + 64 + lane);  // with the count: one round trip
             if (n & END) break;
             valid = lane < n;
@@ -659,7 +676,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             tl_avail = STAT_CLK();
 #endif
             const uint32_t slot = itail % R;
-            const uint32_t n = ictl[2 + slot];
+            const uint32_t n = __builtin_amdgcn_readfirstlane(ictl[2 + slot]);
             if (n & END) break;
             const uint32_t *sd = idata + (size_t)slot * NF * 64;
             valid = lane < n;
@@ -676,7 +693,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
         // idle flush (global link): the consumer's tail, loaded now and used after the
         // candidate loop, so its round trip overlaps this batch's work
         uint32_t tail_async = 0;
-        const bool tail_issued = (a.flush & 2u) && g_out && ofill != 0;
+        const bool tail_issued = (gflush & 2u) && g_out && ofill != 0;
         if (tail_issued) tail_async = g_ld(gout_head + LCTL / 2);
         // bucket indices: packed into s_idx by k_gather_sorted (one binary search per container
         // instead of one per container and stage), else searched here
@@ -819,13 +836,13 @@ k_ffd_pipe(const PipeArgs a_arg) {
                     break;
                 }
                 if (fwd) {
-                    uint32_t *sd = gout_data + (size_t)((ohead + (pos >= 64 ? 1 : 0)) % gslots) * LSLOT;
+                    uint32_t *sd = gout_data + (size_t)GSLOT(ohead + (pos >= 64 ? 1 : 0)) * LSLOT;
                     g_st(sd + 64 + (pos & 63u), idx);
                 }
                 if (ofill + f >= 64) {
-                    if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, 64u);
+                    if (lane == 0) g_st(gout_data + (size_t)GSLOT(ohead) * LSLOT, 64u);
                     ohead++;
-                    if (++opend >= a.publish) {
+                    if (unbounded_only ? (ohead & a.pub_mask) == 0 : ++opend >= a.publish) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         if (lane == 0) g_st(gout_head, ohead);
                         opend = 0;
@@ -837,7 +854,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             }
             // the consumer publishes slot j's index when it takes slot j (tail lags by one)
             if (tail_issued && ofill && __builtin_amdgcn_readfirstlane(tail_async) + 1u >= ohead) {
-                if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, ofill);
+                if (lane == 0) g_st(gout_data + (size_t)GSLOT(ohead) * LSLOT, ofill);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 ohead++;
                 if (lane == 0) g_st(gout_head, ohead);
@@ -885,7 +902,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             }
         }
         // idle flush (see the global link above): the consumer has taken every published slot
-        if ((a.flush & 1u) && ofill && lds_acq(&octl[1]) == ohead) {
+        if ((gflush & 1u) && ofill && lds_acq(&octl[1]) == ohead) {
             octl[2 + ohead % R] = ofill;
             ohead++;
             lds_rel(&octl[0], ohead);
@@ -909,12 +926,12 @@ k_ffd_pipe(const PipeArgs a_arg) {
     if (g_out && !lds_acq(abort_flag) &&
         (!gbounded || gring_wait(gout_head + LCTL / 2, ohead + 2, gslots, otail_seen, a, abort_flag, lane, st_spin_out))) {
         if (ofill) {
-            if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, ofill);
+            if (lane == 0) g_st(gout_data + (size_t)GSLOT(ohead) * LSLOT, ofill);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ohead++;
             if (lane == 0) g_st(gout_head, ohead);
         }
-        if (lane == 0) g_st(gout_data + (size_t)(ohead % gslots) * LSLOT, END);
+        if (lane == 0) g_st(gout_data + (size_t)GSLOT(ohead) * LSLOT, END);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ohead++;
         if (lane == 0) g_st(gout_head, ohead);
@@ -965,6 +982,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
     (void)ck_t0; (void)ck_in; (void)ck_pre; (void)ck_cand; (void)ck_fwd; (void)ck_wait; (void)ck_gx; (void)ck_gu;
     (void)st_queues; (void)st_touched;
     (void)st_spin_in; (void)st_spin_out; (void)st_visits; (void)st_checks; (void)st_hits; (void)st_batches;
+#undef GSLOT
     // write the tile's node state back (registers -> HBM)
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
@@ -1655,6 +1673,9 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     {
         const int64_t pv = fp_opt(c, FP_OPT_LINK_PUBLISH, 32);
         a.publish = geo.bounded ? 1u : (uint32_t)(pv < 1 ? 1 : pv > 1024 ? 1024 : pv);
+        uint32_t p2 = 1;
+        while (p2 * 2 <= a.publish) p2 *= 2;
+        a.pub_mask = p2 - 1;
     }
     // bucket thresholds (device; fp_place.hip k_thresholds chooses them -- any ascending choice
     // with T0 = 0 is exact, it only decides how tight the candidate masks are)
@@ -1679,8 +1700,9 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     }
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
-    int rc = (wide12_big(S, W, G) ? kLaunchWide12Big : wide ? kLaunchWide[G / 4] : kLaunch[G])(st, (unsigned)(S * B),
-                                                                                               W * 64, lds, a);
+    // the six-wave kernel is compiled for unbounded links only (see the kernel)
+    const bool big = wide12_big(S, W, G) && !geo.bounded && !(a.flush & 2u);
+    int rc = (big ? kLaunchWide12Big : wide ? kLaunchWide[G / 4] : kLaunch[G])(st, (unsigned)(S * B), W * 64, lds, a);
     if (rc) return rc;
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
