@@ -11,7 +11,10 @@
 namespace fpp {
 
 // re-test of a group's queue after its first miss: batch corners of at most this many nodes
-constexpr uint32_t REFILTER_MAX = 16;
+#ifndef FPP_REFILTER_MAX
+#define FPP_REFILTER_MAX 16
+#endif
+constexpr uint32_t REFILTER_MAX = FPP_REFILTER_MAX;
 
 __device__ __forceinline__ uint64_t fpp_uniform64(uint64_t x) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
