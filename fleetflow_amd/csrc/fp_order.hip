@@ -214,6 +214,7 @@ __global__ void k_lvl_final(const uint32_t *__restrict__ indeg, uint32_t V, uint
 // nothing can be pushed again.  One monitor lane checks it and raises `fin`.
 constexpr uint32_t kShards = 8;           // queues (blocks b and b+8 share an XCD)
 constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B lines)
+constexpr uint32_t kMaxLevelWord = 26 * kCtlStride;  // ctl word: the largest level the schedule wrote
 constexpr uint64_t kQEmpty = ~0ull;
 // edges left at which the wave expands a vertex together, and edges a lane relaxes per round
 // (config 5: 16 / 1 0.775 ms; cooperative at 8 0.823, at 32 0.779; 2 edges per lane 0.877;
@@ -669,7 +670,7 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         else __builtin_amdgcn_s_sleep(8);
     }
     for (int o = 32; o > 0; o >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor((int)my_max, o));
-    if (lane == 0 && my_max) atomicMax(&ctl[26 * kCtlStride], my_max);
+    if (lane == 0 && my_max) atomicMax(&ctl[kMaxLevelWord], my_max);
 }
 
 // level -> sort keys; vertices never finished (cycle members and everything behind
@@ -681,14 +682,14 @@ __global__ void k_lvl_async_final(uint32_t V, const uint32_t *__restrict__ ctl, 
                                   uint32_t *__restrict__ ck,
                                   const uint32_t *__restrict__ bad, uint32_t *__restrict__ ncyc_out) {
     if (*bad) return;
-    const uint32_t maxl = ctl[26 * kCtlStride];
+    const uint32_t maxl = ctl[kMaxLevelWord];
     const uint32_t cyc_key = (maxl > 1 ? maxl : 1u) + 1u;
     if (blockIdx.x == 0 && threadIdx.x == 0) *ck = cyc_key;
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool cyc = v < V && level[v] == FP_NONE;
     if (v < V) {
         keys[v] = cyc ? cyc_key : level[v];
-        vals[v] = (uint32_t)v;  // the radix fallback's values (the counting sort's scratch)
+        if (vals) vals[v] = (uint32_t)v;  // the radix fallback's values (null for the counting sort)
     }
     const uint64_t m = __ballot(cyc);
     if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) {
@@ -717,8 +718,7 @@ struct CsPass {
     uint32_t sh, nb, nbits;  // digit shift, bins (digits < nb), bits the match masks test
     bool active, last;
 };
-__device__ __forceinline__ CsPass cs_pass(uint32_t p, const uint32_t *ck) {
-    const uint32_t kmax = *ck;
+__device__ __forceinline__ CsPass cs_pass_k(uint32_t p, uint32_t kmax) {
     const uint32_t bits = kmax ? 32u - (uint32_t)__builtin_clz(kmax) : 1u;
     const uint32_t need = (bits + CS_BITS - 1u) / CS_BITS;
     CsPass c;
@@ -729,21 +729,53 @@ __device__ __forceinline__ CsPass cs_pass(uint32_t p, const uint32_t *ck) {
     c.nbits = c.nb > 1u ? 32u - (uint32_t)__builtin_clz(c.nb - 1u) : 0u;
     return c;
 }
+__device__ __forceinline__ CsPass cs_pass(uint32_t p, const uint32_t *ck) { return cs_pass_k(p, *ck); }
+// The asynchronous levelizer sorts its levels in place of keys (LvlMap): pass 0 reads level[] and
+// sorts a CYCLE vertex (FP_NONE) under the cycle key, max(largest level, 1) + 1, which k_cs_hist
+// derives from the schedule's largest level and publishes for the later kernels (no key array
+// and no separate key kernel).
+struct LvlMap {
+    const uint32_t *maxl;  // null: the keys are plain keys; else the async schedule's largest level
+    uint32_t *ncyc, *ncyc_out;  // cycle counts (k_cs_hist, pass 0)
+};
+__device__ __forceinline__ uint32_t cs_key(uint32_t k, uint32_t ckey) { return k == FP_NONE ? ckey : k; }
 __device__ __forceinline__ uint32_t cs_digit(uint32_t key, const CsPass &c) {
     return min(c.last ? key >> c.sh : (key >> c.sh) & (CS_BINS - 1u), c.nb - 1u);
 }
 
 __global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t p,
-                                                  const uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
-                                                  uint32_t *__restrict__ hist) {
+                                                  uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
+                                                  uint32_t *__restrict__ hist, LvlMap lm) {
     if (*bad) return;
-    const CsPass c = cs_pass(p, ck);
+    const bool map = lm.maxl && p == 0;
+    uint32_t ckey = 0;
+    if (map) {
+        const uint32_t maxl = *lm.maxl;
+        ckey = (maxl > 1 ? maxl : 1u) + 1u;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *ck = ckey;  // the later kernels read it
+    }
+    const CsPass c = map ? cs_pass_k(p, ckey) : cs_pass(p, ck);
     if (!c.active) return;
     __shared__ uint32_t h[CS_BINS];
     for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) h[b] = 0;
     __syncthreads();
     const size_t t0 = (size_t)blockIdx.x * CS_TILE;
-    for (uint32_t i = threadIdx.x; i < CS_TILE && t0 + i < V; i += blockDim.x) atomicAdd(&h[cs_digit(keys[t0 + i], c)], 1u);
+    uint32_t ncy = 0;
+    for (uint32_t i = threadIdx.x; i < CS_TILE && t0 + i < V; i += blockDim.x) {
+        uint32_t k = keys[t0 + i];
+        if (map) {
+            ncy += k == FP_NONE ? 1u : 0u;
+            k = cs_key(k, ckey);
+        }
+        atomicAdd(&h[cs_digit(k, c)], 1u);
+    }
+    if (map) {  // the cycle vertices: one atomic per wave that has any
+        for (int o = 32; o > 0; o >>= 1) ncy += (uint32_t)__shfl_xor((int)ncy, o);
+        if ((threadIdx.x & 63) == 0 && ncy) {
+            atomicAdd(lm.ncyc, ncy);
+            if (lm.ncyc_out) atomicAdd(lm.ncyc_out, ncy);
+        }
+    }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) hist[(size_t)blockIdx.x * c.nb + b] = h[b];
 }
@@ -756,19 +788,34 @@ __global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t
     const uint32_t nb = c.nb;
     __shared__ uint32_t tot[CS_BINS];
     const uint32_t b = threadIdx.x;  // one bin per thread (nb <= CS_BINS = blockDim)
+    constexpr uint32_t REG_TILES = 64;  // up to 1M keys: the bin's counts stay in registers
+    uint32_t x[REG_TILES];
     uint32_t run = 0;
-    if (b < nb)
-        for (uint32_t t0 = 0; t0 < ntiles; t0 += 8) {  // 8 independent loads in flight
-            uint32_t x[8];
+    const bool in_regs = ntiles <= REG_TILES;
+    if (b < nb) {
+        if (in_regs) {  // every load in flight at once, one round trip; the prefix in registers
 #pragma unroll
-            for (uint32_t j = 0; j < 8; ++j) x[j] = t0 + j < ntiles ? hist[(size_t)(t0 + j) * nb + b] : 0u;
+            for (uint32_t t = 0; t < REG_TILES; ++t) x[t] = t < ntiles ? hist[(size_t)t * nb + b] : 0u;
 #pragma unroll
-            for (uint32_t j = 0; j < 8; ++j)
-                if (t0 + j < ntiles) {
-                    hist[(size_t)(t0 + j) * nb + b] = run;
-                    run += x[j];
-                }
+            for (uint32_t t = 0; t < REG_TILES; ++t) {
+                const uint32_t y = x[t];
+                x[t] = run;
+                run += y;
+            }
+        } else {
+            for (uint32_t t0 = 0; t0 < ntiles; t0 += 8) {  // 8 independent loads in flight
+                uint32_t y[8];
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) y[j] = t0 + j < ntiles ? hist[(size_t)(t0 + j) * nb + b] : 0u;
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j)
+                    if (t0 + j < ntiles) {
+                        hist[(size_t)(t0 + j) * nb + b] = run;
+                        run += y[j];
+                    }
+            }
         }
+    }
     tot[b] = b < nb ? run : 0u;
     __syncthreads();
     // exclusive scan of tot[] (Hillis-Steele in LDS)
@@ -779,8 +826,15 @@ __global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t
         __syncthreads();
     }
     const uint32_t base = tot[b] - run;  // inclusive - own
-    if (b < nb)
-        for (uint32_t t = 0; t < ntiles; ++t) hist[(size_t)t * nb + b] += base;
+    if (b < nb) {
+        if (in_regs) {
+#pragma unroll
+            for (uint32_t t = 0; t < REG_TILES; ++t)
+                if (t < ntiles) hist[(size_t)t * nb + b] = x[t] + base;
+        } else {
+            for (uint32_t t = 0; t < ntiles; ++t) hist[(size_t)t * nb + b] += base;
+        }
+    }
 }
 
 __device__ __forceinline__ uint64_t cs_match(uint32_t v, bool valid, uint32_t nbits) {
@@ -799,8 +853,10 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
                                                      uint32_t V, uint32_t p, const uint32_t *__restrict__ ck,
                                                      const uint32_t *__restrict__ bad, const uint32_t *__restrict__ off,
                                                      uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
-                                                     uint32_t *__restrict__ vout) {
+                                                     uint32_t *__restrict__ vout, bool map) {
     if (*bad) return;
+    map = map && p == 0;  // levels as keys (LvlMap): *ck is the cycle key, written by k_cs_hist
+    const uint32_t ckey = map ? *ck : 0u;
     const CsPass c = cs_pass(p, ck);
     if (!c.active) return;
     const uint32_t nb = c.nb;
@@ -812,7 +868,10 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
     const size_t t0 = (size_t)blockIdx.x * CS_TILE;
     const uint32_t slice = CS_TILE / CS_WAVES;
     const size_t s0 = t0 + (size_t)w * slice;
-    for (uint32_t i = lane; i < slice && s0 + i < V; i += 64) atomicAdd(&wh[w][cs_digit(keys[s0 + i], c)], 1u);
+    for (uint32_t i = lane; i < slice && s0 + i < V; i += 64) {
+        const uint32_t k = keys[s0 + i];
+        atomicAdd(&wh[w][cs_digit(map ? cs_key(k, ckey) : k, c)], 1u);
+    }
     __syncthreads();
     for (uint32_t b = t; b < nb; b += blockDim.x) {  // per bin: wave offsets in wave order
         uint32_t run = off[(size_t)blockIdx.x * nb + b];
@@ -826,7 +885,7 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
     for (uint32_t i0 = 0; i0 < slice && s0 + i0 < V; i0 += 64) {
         const size_t v = s0 + i0 + lane;
         const bool valid = i0 + lane < slice && v < V;
-        const uint32_t key = valid ? keys[v] : 0u;
+        const uint32_t key = valid ? (map ? cs_key(keys[v], ckey) : keys[v]) : 0u;
         const uint32_t k = valid ? cs_digit(key, c) : 0u;
         const uint32_t x = valid ? (vals ? vals[v] : (uint32_t)v) : 0u;
         const uint64_t m = cs_match(k, valid, c.nbits);
@@ -914,8 +973,8 @@ int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
 // 32 key bits (vals = the identity, k_lvl_*final).  No read-back either way.  Scratch: two
 // (key, vertex) pairs, kb[0]/vb[0] and kb[1]/vb[1].
 static int level_sort(hipStream_t st, bool counting, uint32_t *keys, uint32_t *const kb[2], uint32_t *const vb[2],
-                      uint32_t *order, uint32_t V, const uint32_t *ck, const uint32_t *bad, void *tmp,
-                      size_t sort_tmp, uint32_t *cs_hist) {
+                      uint32_t *order, uint32_t V, uint32_t *ck, const uint32_t *bad, void *tmp,
+                      size_t sort_tmp, uint32_t *cs_hist, LvlMap lm = LvlMap{nullptr, nullptr, nullptr}) {
     const uint32_t ntiles = (uint32_t)(((size_t)V + CS_TILE - 1) / CS_TILE);
     if (counting && ntiles <= CS_MAX_TILES) {
         // the largest key either schedule can produce: the async cycle key is max(level, 1) + 1 <=
@@ -924,11 +983,12 @@ static int level_sort(hipStream_t st, bool counting, uint32_t *keys, uint32_t *c
         for (uint32_t p = 0; p < passes; ++p) {
             const uint32_t *ik = p ? kb[(p - 1) & 1] : keys;
             const uint32_t *iv = p ? vb[(p - 1) & 1] : nullptr;
-            k_cs_hist<<<ntiles, 1024, 0, st>>>(ik, V, p, ck, bad, cs_hist);
+            k_cs_hist<<<ntiles, 1024, 0, st>>>(ik, V, p, ck, bad, cs_hist, lm);
             FP_HIP(hipGetLastError());
             k_cs_scan<<<1, CS_BINS, 0, st>>>(cs_hist, ntiles, p, ck, bad);
             FP_HIP(hipGetLastError());
-            k_cs_scatter<<<ntiles, 1024, 0, st>>>(ik, iv, V, p, ck, bad, cs_hist, order, kb[p & 1], vb[p & 1]);
+            k_cs_scatter<<<ntiles, 1024, 0, st>>>(ik, iv, V, p, ck, bad, cs_hist, order, kb[p & 1], vb[p & 1],
+                                                  lm.maxl != nullptr);
             FP_HIP(hipGetLastError());
         }
         return FP_OK;
@@ -1038,9 +1098,17 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         }
         // the cycle key (from the largest level seen) is computed on the device: no read-back; the
         // cycle count goes straight to the caller's word (zeroed by k_lvl_zero)
-        k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, actl, level, keys, vals, ncyc, ck, bad, n_cycle_dev);
-        FP_HIP(hipGetLastError());
-        if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
+        const bool cs_path = counting && (((size_t)V + CS_TILE - 1) / CS_TILE) <= CS_MAX_TILES;
+        if (cs_path) {
+            // the counting sort reads the levels themselves (LvlMap): cycle key, keys and cycle count
+            // come out of its first pass
+            const LvlMap lm{actl + kMaxLevelWord, ncyc, n_cycle_dev};
+            if ((rc = level_sort(st, counting, level, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist, lm))) return rc;
+        } else {
+            k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, actl, level, keys, vals, ncyc, ck, bad, n_cycle_dev);
+            FP_HIP(hipGetLastError());
+            if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
+        }
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
     }
