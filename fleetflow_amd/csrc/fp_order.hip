@@ -1074,8 +1074,12 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         uint32_t *qflag = (uint32_t *)((char *)c->lvl_q + c->lvl_q_cap - 256);
         // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
         const bool pk = V < (1u << 24);
-        const unsigned zg = blocks_for(qbytes / 16, 256) < 8192 ? blocks_for(qbytes / 16, 256) : 8192;
-        k_lvl_zero<<<zg, 256, 0, st>>>(V, indeg, ncyc, actl, n_cycle_dev, (uint4 *)Q, qbytes / 16, qflag);
+        const unsigned zg = blocks_for((c->lvl_q_cap - 256) / 16, 256) < 8192 ? blocks_for((c->lvl_q_cap - 256) / 16, 256) : 8192;
+        // "clean" covers the WHOLE buffer: a dirty buffer is refilled to its capacity, not to this
+        // call's queue size, so a later call with a larger graph (a larger queue in the same
+        // buffer) never reads slots an earlier, smaller call left unfilled
+        const size_t qfill = c->lvl_q_cap - 256;
+        k_lvl_zero<<<zg, 256, 0, st>>>(V, indeg, ncyc, actl, n_cycle_dev, (uint4 *)Q, qfill / 16, qflag);
         FP_HIP(hipGetLastError());
         const size_t nmax = V + 1 > E ? (size_t)V + 1 : E;
         k_indeg_check<<<blocks_for(nmax, 256) < 8192 ? blocks_for(nmax, 256) : 8192, 256, 0, st>>>(

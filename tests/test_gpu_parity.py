@@ -790,8 +790,8 @@ def test_levelize_sync_cycle_key_pass_boundary(V, planner, O):
 def test_levelize_queue_reuse_across_calls(planner, O):
     """The asynchronous levelizer keeps its work queues between calls and refills them only when
     the last call left them dirty (fp_order.hip kQClean): alternate graphs, a corrupt CSR (queues
-    dirty), an edgeless graph (no async kernel) and bigger graphs (the buffer grows), every result
-    against the oracle."""
+    dirty), an edgeless graph (no async kernel), bigger graphs (the buffer grows) and bigger graphs
+    that still fit the buffer, every result against the oracle."""
     from fleetflow_amd._lib import FleetplaceError
 
     def dag(V, E, seed):
@@ -802,9 +802,12 @@ def test_levelize_queue_reuse_across_calls(planner, O):
         hd = (rng.random(V) < 0.7).astype(np.uint8)
         return rp, col, hd
 
-    graphs = [dag(5_000, 20_000, 1), dag(40_000, 90_000, 2), "corrupt", dag(5_000, 20_000, 1),
-              (np.zeros(2_001, np.uint32), np.zeros(0, np.uint32), np.ones(2_000, np.uint8)),
-              dag(120_000, 300_000, 3), dag(40_000, 90_000, 2)]
+    # 40k -> 45k: a larger queue inside the same buffer (its capacity has 25 % slack), whose tail
+    # the 40k call never used -- "clean" must cover the whole buffer (the plan_stage 513 -> 700
+    # services case that once read unfilled slots and hung)
+    graphs = [dag(5_000, 20_000, 1), dag(40_000, 90_000, 2), dag(45_000, 100_000, 4), "corrupt",
+              dag(5_000, 20_000, 1), (np.zeros(2_001, np.uint32), np.zeros(0, np.uint32), np.ones(2_000, np.uint8)),
+              dag(120_000, 300_000, 3), dag(40_000, 90_000, 2), dag(140_000, 320_000, 5)]
     for g in graphs:
         if isinstance(g, str):  # "corrupt": col out of range
             with pytest.raises(FleetplaceError):
