@@ -14,6 +14,7 @@
 //     with the levels' CYCLE gate, the node table updated in place.
 // Larger stages run the general kernels through the same host calls as before.
 #include "fp_internal.h"
+#include <chrono>
 #include "fp_small.h"
 #include <string.h>
 #include <vector>
@@ -46,6 +47,12 @@ inline size_t plan_small_words(uint32_t V, uint32_t E, uint32_t N, bool place) {
                2 * words4((size_t)V * 4);
     if (place) w += 4 * words4((size_t)V * 4) + 4 * words4((size_t)N * 4) + words4(N) + words4((size_t)V * 4);
     return w;
+}
+
+// The completion word of k_plan_small: written last, with system-scope release, in mapped host
+// memory; fp_plan_stage polls it instead of synchronising the stream
+__device__ __forceinline__ void plan_small_done(uint32_t *err, uint32_t v) {
+    __hip_atomic_store(err, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(1024) void k_plan_small(const PlanSmallArgs a) {
@@ -90,7 +97,7 @@ __global__ __launch_bounds__(1024) void k_plan_small(const PlanSmallArgs a) {
     // A2: levels and the start order (the CSR check first: a corrupt CSR writes nothing else)
     const uint32_t nc = fps::ls_levels(rp, col, hd, V, E, ks, lv, od);
     if (nc == FP_NONE) {
-        if (t == 0) *a.err = (uint32_t)(-FP_ECORRUPT);
+        if (t == 0) plan_small_done(a.err, (uint32_t)(-FP_ECORRUPT));
         return;  // uniform
     }
 
@@ -186,7 +193,10 @@ __global__ __launch_bounds__(1024) void k_plan_small(const PlanSmallArgs a) {
             a.cu_out[i] = cu[i];
         }
     }
-    if (t == 0) *a.err = 0u;
+    // every thread's results reach host memory before the completion word (the host polls it)
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) plan_small_done(a.err, 0u);
 }
 
 // the general path: the separate host-pointer calls into temporaries, committed only when all
@@ -317,8 +327,19 @@ extern "C" int fp_plan_stage(fp_ctx *c, const fp_graph *g, const fp_containers *
     k_plan_small<<<1, 1024, lds, c->stream>>>(a);
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_LEVEL, ev);
-    FP_HIP(hipStreamSynchronize(c->stream));
-    const uint32_t e = h[o_err];
+    // poll the completion word (mapped, coherent host memory); the stream synchronisation is only
+    // the fallback for a kernel that has not finished after ~20 ms, and the path when profiling
+    volatile uint32_t *done = h + o_err;
+    bool seen = false;
+    if (!c->profile) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0;; ++spin) {
+            if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != 0xFFFFFFFFu) { seen = true; break; }
+            if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+        }
+    }
+    if (!seen) FP_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t e = __atomic_load_n(done, __ATOMIC_ACQUIRE);
     if (e == 0xFFFFFFFFu) return FP_EDEVICE;  // the kernel did not finish
     if (e) return -(int)e;
     memcpy(perm_out, h + o_perm, (size_t)V * 4);
