@@ -24,7 +24,8 @@ FP_OPT_AUTO = -1
 OPTIONS = {"pipe_w": 0, "pipe_seg": 1, "pipe_r": 2, "pipe_lag": 3, "link_slots": 4, "link_bounded": 5,
            "pipe_flush": 6, "spin_ticks": 7, "kpack": 8, "scen_sort": 9, "segsort": 10, "systolic": 11,
            "levelize_sync": 12, "systolic_extra": 13, "screen": 14, "payload_lds": 15, "systolic_valu": 16, "link_publish": 17,
-           "level_sort": 18, "level_small": 19, "pipe_prio": 20}
+           "level_sort": 18, "level_small": 19, "pipe_prio": 20,
+           "indeg_bin": 21}
 # fp_place_geometry out[] (fleetplace.h FP_GEOM_*)
 GEOM_FIELDS = ("groups", "stages", "segments", "ring", "lag", "link_slots", "bounded", "resident", "systolic")
 

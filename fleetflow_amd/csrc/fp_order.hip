@@ -302,6 +302,108 @@ __global__ void k_indeg_check(const uint32_t *__restrict__ row_ptr, const uint32
     }
 }
 
+// The in-degrees without global atomics (round 5; FP_OPT_INDEG_BIN = 0 keeps k_indeg_check).
+// k_indeg_check's 1.75M atomicAdds on random words run at the memory side, one request per lane
+// (config 5: 67 us).  Here the edges are binned by child range instead: k_indeg_bin sorts each
+// 4096-edge slice by bucket (child >> shift, at most kBinMaxB buckets) in LDS and writes it back in
+// place with the bucket starts (transposed: offt[b * nwg + slice], row B = the slice's total);
+// k_indeg_hist counts one bucket's children in LDS from every slice's run and stores its range's
+// in-degrees coalesced, beside the row_ptr checks.
+constexpr uint32_t kBinT = 256, kBinPer = 16, kBinSlice = kBinT * kBinPer, kBinMaxB = 1024;
+constexpr uint32_t kBinMinShift = 12, kBinMaxShift = 14;  // bucket ranges 4096 .. 16384 vertices
+constexpr uint32_t kHistT = 1024;
+
+__global__ __launch_bounds__(kBinT) void k_indeg_bin(const uint32_t *__restrict__ col, uint32_t V, uint32_t E,
+                                                     uint32_t shift, uint32_t B, uint32_t nwg,
+                                                     uint32_t *__restrict__ binned, uint32_t *__restrict__ offt,
+                                                     uint32_t *__restrict__ err, uint32_t *__restrict__ bad,
+                                                     uint32_t *__restrict__ qflag) {
+    __shared__ uint32_t cnt[kBinMaxB + 1];
+    __shared__ uint32_t wsum[kBinT / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const size_t e0 = (size_t)blockIdx.x * kBinSlice;
+    if (blockIdx.x == 0 && t == 0) *qflag = 0u;
+    for (uint32_t b = t; b < 4 * kBinT; b += kBinT) cnt[b] = 0u;
+    __syncthreads();
+    uint32_t v[kBinPer], r[kBinPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kBinPer; ++k) {
+        const size_t i = e0 + k * kBinT + t;
+        v[k] = i < E ? col[i] : ~0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kBinPer; ++k) {
+        const size_t i = e0 + k * kBinT + t;
+        if (i < E && v[k] >= V) lv_corrupt(err, bad);
+        if (v[k] < V) r[k] = atomicAdd(&cnt[v[k] >> shift], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of the bucket counts: thread t holds buckets [4t, 4t + 4)
+    uint32_t c4[4], s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        c4[j] = cnt[4 * t + j];
+        s += c4[j];
+    }
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if ((int)lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t run = inc - s;
+    for (uint32_t w = 0; w < wv; ++w) run += wsum[w];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        cnt[4 * t + j] = run;
+        run += c4[j];
+    }
+    if (t == kBinT - 1) cnt[B] = run;  // the slice's total (buckets >= B count nothing)
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kBinPer; ++k)
+        if (v[k] < V) binned[e0 + cnt[v[k] >> shift] + r[k]] = v[k];
+    for (uint32_t b = t; b <= B; b += kBinT) offt[(size_t)b * nwg + blockIdx.x] = cnt[b];
+}
+
+// one workgroup per bucket: split = threads per slice run (a power of two, nwg * split <= kHistT
+// where the slices are few), each thread four loads in flight
+__global__ __launch_bounds__(kHistT) void k_indeg_hist(const uint32_t *__restrict__ binned,
+                                                       const uint32_t *__restrict__ offt, uint32_t nwg,
+                                                       uint32_t split, uint32_t shift, uint32_t V, uint32_t E,
+                                                       const uint32_t *__restrict__ row_ptr,
+                                                       uint32_t *__restrict__ indeg, uint32_t *__restrict__ err,
+                                                       uint32_t *__restrict__ bad) {
+    extern __shared__ uint32_t h[];
+    const uint32_t t = threadIdx.x, b = blockIdx.x;
+    const uint32_t v0 = b << shift, n = min(V - v0, 1u << shift);
+    for (uint32_t i = t; i < n; i += kHistT) h[i] = 0u;
+    __syncthreads();
+    const uint32_t part = t & (split - 1);
+    for (uint32_t sl = t / split; sl < nwg; sl += kHistT / split) {
+        const uint32_t *p = binned + (size_t)sl * kBinSlice;
+        const uint32_t a = offt[(size_t)b * nwg + sl] + part, z = offt[(size_t)(b + 1) * nwg + sl];
+        for (uint32_t i = a; i < z; i += 4 * split) {
+            uint32_t x[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) x[k] = i + k * split < z ? p[i + k * split] : ~0u;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+                if (x[k] != ~0u) atomicAdd(&h[x[k] - v0], 1u);
+        }
+    }
+    __syncthreads();
+    if (b == 0 && t == 0 && (row_ptr[0] != 0 || row_ptr[V] != E)) lv_corrupt(err, bad);
+#pragma unroll 4
+    for (uint32_t i = t; i < n; i += kHistT) {
+        const uint32_t v = v0 + i;
+        indeg[v] = h[i];
+        if (row_ptr[v + 1] < row_ptr[v]) lv_corrupt(err, bad);
+    }
+}
+
 // The vertex states and the source queue items (blocks [0, vblocks): one vertex per thread) beside
 // the edge records (the other blocks, grid-stride over the edges) in one launch
 __global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
@@ -1027,7 +1129,14 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
     }
-    const size_t async_ws = level_sync ? 0 : (size_t)V * 8 + (size_t)E * 16 * kHops + kCtlWords * 4;
+    // the binned in-degree count (k_indeg_bin / k_indeg_hist) when the buckets fit its tables
+    uint32_t bin_shift = kBinMinShift;
+    while (bin_shift < kBinMaxShift && ((V + (1u << bin_shift) - 1) >> bin_shift) > kBinMaxB) ++bin_shift;
+    const uint32_t bin_b = (uint32_t)(((size_t)V + (1u << bin_shift) - 1) >> bin_shift);
+    const uint32_t bin_nwg = (uint32_t)(((size_t)E + kBinSlice - 1) / kBinSlice);
+    const bool binned_indeg = !level_sync && E && bin_b <= kBinMaxB && fp_opt(c, FP_OPT_INDEG_BIN, 1) != 0;
+    const size_t bin_ws = binned_indeg ? (size_t)E * 4 + (size_t)(bin_b + 1) * bin_nwg * 4 + 512 : 0;
+    const size_t async_ws = level_sync ? 0 : (size_t)V * 8 + (size_t)E * 16 * kHops + kCtlWords * 4 + bin_ws;
     const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 : 0;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + async_ws + cs_ws + 23 * 256);
     if (rc) return rc;
@@ -1079,12 +1188,28 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         // call's queue size, so a later call with a larger graph (a larger queue in the same
         // buffer) never reads slots an earlier, smaller call left unfilled
         const size_t qfill = c->lvl_q_cap - 256;
-        k_lvl_zero<<<zg, 256, 0, st>>>(V, indeg, ncyc, actl, n_cycle_dev, (uint4 *)Q, qfill / 16, qflag);
+        // (the binned count stores every in-degree itself: no zeroing)
+        k_lvl_zero<<<zg, 256, 0, st>>>(binned_indeg ? 0u : V, indeg, ncyc, actl, n_cycle_dev, (uint4 *)Q, qfill / 16,
+                                       qflag);
         FP_HIP(hipGetLastError());
         const size_t nmax = V + 1 > E ? (size_t)V + 1 : E;
-        k_indeg_check<<<blocks_for(nmax, 256) < 8192 ? blocks_for(nmax, 256) : 8192, 256, 0, st>>>(
-            g->row_ptr, g->col, V, E, indeg, c->d_err, bad, qflag);
-        FP_HIP(hipGetLastError());
+        if (binned_indeg) {
+            uint32_t *binned = (uint32_t *)fp_ws_take(c, (size_t)E * 4);
+            uint32_t *offt = (uint32_t *)fp_ws_take(c, (size_t)(bin_b + 1) * bin_nwg * 4);
+            if (!binned || !offt) return FP_ENOMEM;
+            k_indeg_bin<<<bin_nwg, kBinT, 0, st>>>(g->col, V, E, bin_shift, bin_b, bin_nwg, binned, offt, c->d_err, bad,
+                                                   qflag);
+            FP_HIP(hipGetLastError());
+            uint32_t split = 1;
+            while (split < 16 && (size_t)bin_nwg * split * 2 <= kHistT) split *= 2;
+            k_indeg_hist<<<bin_b, kHistT, (4u << bin_shift), st>>>(binned, offt, bin_nwg, split, bin_shift, V, E,
+                                                                    g->row_ptr, indeg, c->d_err, bad);
+            FP_HIP(hipGetLastError());
+        } else {
+            k_indeg_check<<<blocks_for(nmax, 256) < 8192 ? blocks_for(nmax, 256) : 8192, 256, 0, st>>>(
+                g->row_ptr, g->col, V, E, indeg, c->d_err, bad, qflag);
+            FP_HIP(hipGetLastError());
+        }
         const uint32_t vblocks = blocks_for(V, 256);
         const unsigned eg = E ? (blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192) : 0u;
         k_lvl_prep<<<vblocks + eg, 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, g->col, V, E, vblocks, level, state, Q,

@@ -313,8 +313,11 @@ class DevBatch:
                        p(self.sched), p(self.assign), p(self.reason), p(self.cost))
 
     def node_snapshot(self):
-        return tuple(t.clone() for t in (self.cf, self.mf, self.lab, self.cu, self.sched))
+        """Copies of the node fields a plan mutates (free cpu, free memory, usage count).
+        labels and schedulable are const inputs at the boundary (include/fleetplace.h:99-101),
+        so they are neither copied nor restored."""
+        return tuple(t.clone() for t in (self.cf, self.mf, self.cu))
 
     def restore_nodes(self, snap):
-        for dst, src in zip((self.cf, self.mf, self.lab, self.cu, self.sched), snap):
+        for dst, src in zip((self.cf, self.mf, self.cu), snap):
             dst.copy_(src)

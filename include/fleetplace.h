@@ -168,7 +168,8 @@ enum fp_option {
     FP_OPT_LEVEL_SORT = 18,   /* levelizer start order: 0 = radix sort, auto = LSD counting sort   */
     FP_OPT_LEVEL_SMALL = 19,  /* 0 = no one-launch levelizer (<= 512 vertices) / legacy order (<= 1024) */
     FP_OPT_PIPE_PRIO = 20,    /* FFD wave priority: 0 off, 1 raised in the group loop, 2 for a batch's work */
-    FP_OPT_COUNT = 21
+    FP_OPT_INDEG_BIN = 21,    /* 0 = levelizer in-degrees by global atomics instead of binned in LDS */
+    FP_OPT_COUNT = 22
 };
 int fp_ctx_set_option(fp_ctx *ctx, int option, int64_t value);
 int fp_ctx_get_option(fp_ctx *ctx, int option, int64_t *value);

@@ -43,6 +43,7 @@ pub const FP_OPT_LINK_PUBLISH: c_int = 17;
 pub const FP_OPT_LEVEL_SORT: c_int = 18;
 pub const FP_OPT_LEVEL_SMALL: c_int = 19;
 pub const FP_OPT_PIPE_PRIO: c_int = 20;
+pub const FP_OPT_INDEG_BIN: c_int = 21;
 pub const FP_GEOM_GROUPS: usize = 0;
 pub const FP_GEOM_STAGES: usize = 1;
 pub const FP_GEOM_SEGMENTS: usize = 2;

@@ -817,3 +817,65 @@ def test_levelize_queue_reuse_across_calls(planner, O):
         level, order, ncyc = planner.levelize(rp, col, hd)
         el, eo, en = O.levelize(rp, col, hd)
         assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
+
+
+@pytest.mark.parametrize("shape", ["one_slice", "ragged_slices", "hub_child", "shift_13", "sequence"])
+def test_levelize_binned_indegree(shape, planner, O):
+    """The asynchronous levelizer's in-degrees binned by child range in LDS (fp_order.hip
+    k_indeg_bin / k_indeg_hist) against the global-atomic count (FP_OPT_INDEG_BIN = 0) and the
+    oracle: fewer edges than one 4096-edge slice, a ragged last slice, one child with 60k parents
+    (one bucket, every slice), a graph whose buckets need 8192-vertex ranges (V > 4M), and the two
+    paths alternating on one context (the binned count stores every in-degree, the other zeroes)."""
+    from fleetflow_amd._lib import FleetplaceError
+    rng = np.random.default_rng(len(shape))
+
+    def rand(V, E):
+        a, b = rng.integers(0, V, E), rng.integers(0, V, E)
+        edges = [(int(x), int(y)) for x, y in zip(a, b) if x < y] + [(V - 3, V - 2), (V - 2, V - 1), (V - 1, V - 3)]
+        rp, col = _csr(V, edges)
+        hd = np.zeros(V, np.uint8)
+        hd[np.unique(col)] = 1
+        return rp, col, hd
+
+    if shape == "one_slice":
+        graphs = [rand(3_000, 2_500)]
+    elif shape == "ragged_slices":
+        graphs = [rand(70_000, 4096 * 9 + 77)]
+    elif shape == "hub_child":
+        V = 80_000
+        edges = [(v, V - 1) for v in range(60_000)] + [(v, v + 1) for v in range(60_000, V - 2)]
+        rp, col = _csr(V, edges)
+        hd = np.zeros(V, np.uint8)
+        hd[np.unique(col)] = 1
+        graphs = [(rp, col, hd)]
+    elif shape == "shift_13":
+        graphs = [rand(4096 * 1024 + 5, 200_000)]
+    else:
+        graphs = [rand(50_000, 120_000), rand(20_000, 30_000), rand(50_000, 120_000)]
+    for i, (rp, col, hd) in enumerate(graphs):
+        el, eo, en = O.levelize(rp, col, hd)
+        for on in ([1, 0] if shape != "sequence" else [i % 2, 1 - i % 2]):
+            planner.set_option("indeg_bin", on)
+            planner.set_option("level_small", 0)
+            try:
+                level, order, ncyc = planner.levelize(rp, col, hd)
+            finally:
+                planner.set_option("indeg_bin")
+                planner.set_option("level_small")
+            assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en, (shape, i, on)
+    # a corrupt CSR on the binned path: a child out of range in the last slice, rows not monotone
+    V = 5_000
+    rp = np.arange(V + 1, dtype=np.uint32)
+    rp[V] = V
+    col = (np.arange(V, dtype=np.uint32) + 1) % V
+    bad_col = col.copy()
+    bad_col[-1] = V + 9
+    bad_rp = rp.copy()
+    bad_rp[2000] = 5
+    for r, c in ((rp, bad_col), (bad_rp, col)):
+        planner.set_option("level_small", 0)
+        try:
+            with pytest.raises(FleetplaceError):
+                planner.levelize(r, c, np.ones(V, np.uint8))
+        finally:
+            planner.set_option("level_small")
