@@ -308,7 +308,8 @@ __global__ void k_indeg_check(const uint32_t *__restrict__ row_ptr, const uint32
 // 4096-edge slice by bucket (child >> shift, at most kBinMaxB buckets) in LDS and writes it back in
 // place with the bucket starts (transposed: offt[b * nwg + slice], row B = the slice's total);
 // k_indeg_hist counts one bucket's children in LDS from every slice's run and stores its range's
-// in-degrees coalesced, beside the row_ptr checks.
+// in-degrees coalesced, beside the row_ptr checks and a 16-B vertex record (its edge range, whether
+// it has one parent) that k_lvl_prep's edge records then take in one random load instead of two lines.
 constexpr uint32_t kBinT = 256, kBinPer = 16, kBinSlice = kBinT * kBinPer, kBinMaxB = 1024;
 constexpr uint32_t kBinMinShift = 12, kBinMaxShift = 14;  // bucket ranges 4096 .. 16384 vertices
 constexpr uint32_t kHistT = 1024;
@@ -374,8 +375,8 @@ __global__ __launch_bounds__(kHistT) void k_indeg_hist(const uint32_t *__restric
                                                        const uint32_t *__restrict__ offt, uint32_t nwg,
                                                        uint32_t split, uint32_t shift, uint32_t V, uint32_t E,
                                                        const uint32_t *__restrict__ row_ptr,
-                                                       uint32_t *__restrict__ indeg, uint32_t *__restrict__ err,
-                                                       uint32_t *__restrict__ bad) {
+                                                       uint32_t *__restrict__ indeg, uint4 *__restrict__ vrec,
+                                                       uint32_t *__restrict__ err, uint32_t *__restrict__ bad) {
     extern __shared__ uint32_t h[];
     const uint32_t t = threadIdx.x, b = blockIdx.x;
     const uint32_t v0 = b << shift, n = min(V - v0, 1u << shift);
@@ -398,9 +399,10 @@ __global__ __launch_bounds__(kHistT) void k_indeg_hist(const uint32_t *__restric
     if (b == 0 && t == 0 && (row_ptr[0] != 0 || row_ptr[V] != E)) lv_corrupt(err, bad);
 #pragma unroll 4
     for (uint32_t i = t; i < n; i += kHistT) {
-        const uint32_t v = v0 + i;
-        indeg[v] = h[i];
-        if (row_ptr[v + 1] < row_ptr[v]) lv_corrupt(err, bad);
+        const uint32_t v = v0 + i, r0 = row_ptr[v], r1 = row_ptr[v + 1], d = h[i];
+        indeg[v] = d;
+        if (r1 < r0) lv_corrupt(err, bad);
+        vrec[v] = make_uint4(r0, r1, d == 1u ? 1u : 0u, 0u);  // k_lvl_prep's edge records: one gather
     }
 }
 
@@ -410,7 +412,7 @@ __global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__res
                            const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t V,
                            uint32_t E, uint32_t vblocks, uint32_t *__restrict__ level, uint64_t *__restrict__ state,
                            uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl, bool pk, uint4 *__restrict__ rec,
-                           const uint32_t *__restrict__ bad) {
+                           const uint4 *__restrict__ vrec, const uint32_t *__restrict__ bad) {
     if (*bad) return;
     if (blockIdx.x < vblocks) {
         const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -439,8 +441,13 @@ __global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__res
     }
     const size_t st = (size_t)(gridDim.x - vblocks) * blockDim.x;
     for (size_t e = (size_t)(blockIdx.x - vblocks) * blockDim.x + threadIdx.x; e < E; e += st) {
-        const uint32_t w = col[e];  // < V: k_indeg_check raised `bad` otherwise
-        rec[e] = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
+        const uint32_t w = col[e];  // < V: k_indeg_check / k_indeg_bin raised `bad` otherwise
+        if (vrec) {
+            const uint4 r = vrec[w];
+            rec[e] = make_uint4(w, r.x, r.y, r.z);
+        } else {
+            rec[e] = make_uint4(w, row_ptr[w], row_ptr[w + 1], indeg[w] == 1u ? 1u : 0u);
+        }
     }
 }
 
@@ -1135,7 +1142,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     const uint32_t bin_b = (uint32_t)(((size_t)V + (1u << bin_shift) - 1) >> bin_shift);
     const uint32_t bin_nwg = (uint32_t)(((size_t)E + kBinSlice - 1) / kBinSlice);
     const bool binned_indeg = !level_sync && E && bin_b <= kBinMaxB && fp_opt(c, FP_OPT_INDEG_BIN, 1) != 0;
-    const size_t bin_ws = binned_indeg ? (size_t)E * 4 + (size_t)(bin_b + 1) * bin_nwg * 4 + 512 : 0;
+    const size_t bin_ws = binned_indeg ? (size_t)E * 4 + (size_t)(bin_b + 1) * bin_nwg * 4 + (size_t)V * 16 + 768 : 0;
     const size_t async_ws = level_sync ? 0 : (size_t)V * 8 + (size_t)E * 16 * kHops + kCtlWords * 4 + bin_ws;
     const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 : 0;
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + async_ws + cs_ws + 23 * 256);
@@ -1193,17 +1200,19 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
                                        qflag);
         FP_HIP(hipGetLastError());
         const size_t nmax = V + 1 > E ? (size_t)V + 1 : E;
+        uint4 *vrec = nullptr;  // per-vertex edge-record halves (binned path)
         if (binned_indeg) {
             uint32_t *binned = (uint32_t *)fp_ws_take(c, (size_t)E * 4);
             uint32_t *offt = (uint32_t *)fp_ws_take(c, (size_t)(bin_b + 1) * bin_nwg * 4);
-            if (!binned || !offt) return FP_ENOMEM;
+            vrec = (uint4 *)fp_ws_take(c, (size_t)V * 16);
+            if (!binned || !offt || !vrec) return FP_ENOMEM;
             k_indeg_bin<<<bin_nwg, kBinT, 0, st>>>(g->col, V, E, bin_shift, bin_b, bin_nwg, binned, offt, c->d_err, bad,
                                                    qflag);
             FP_HIP(hipGetLastError());
             uint32_t split = 1;
             while (split < 16 && (size_t)bin_nwg * split * 2 <= kHistT) split *= 2;
             k_indeg_hist<<<bin_b, kHistT, (4u << bin_shift), st>>>(binned, offt, bin_nwg, split, bin_shift, V, E,
-                                                                    g->row_ptr, indeg, c->d_err, bad);
+                                                                    g->row_ptr, indeg, vrec, c->d_err, bad);
             FP_HIP(hipGetLastError());
         } else {
             k_indeg_check<<<blocks_for(nmax, 256) < 8192 ? blocks_for(nmax, 256) : 8192, 256, 0, st>>>(
@@ -1213,7 +1222,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         const uint32_t vblocks = blocks_for(V, 256);
         const unsigned eg = E ? (blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192) : 0u;
         k_lvl_prep<<<vblocks + eg, 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, g->col, V, E, vblocks, level, state, Q,
-                                                 actl, pk, erec, bad);
+                                                 actl, pk, erec, vrec, bad);
         FP_HIP(hipGetLastError());
         if (E) {
             if (pk) {  // the hops are read only with packed queue entries
