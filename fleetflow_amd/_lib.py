@@ -84,8 +84,9 @@ SIGNATURES = {
     "fp_place": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p, u8p]),
     "fp_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),
     "fp_feasibility": (ct.c_int, [vp, ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p, u64p]),
-    "fp_plan_stage": (ct.c_int, [vp, ct.POINTER(FpGraph), ct.POINTER(FpContainers), ct.POINTER(FpNodes), u32p, u32p,
-                                 u32p, u32p, u32p, u32p, u32p, u8p]),
+    # output arrays as plain addresses (vp): a 3-service stage's call is on the config-1 clock
+    "fp_plan_stage": (ct.c_int, [vp, ct.POINTER(FpGraph), ct.POINTER(FpContainers), ct.POINTER(FpNodes), vp, vp,
+                                 vp, u32p, vp, vp, vp, vp]),
     "fp_dev_legacy_order": (ct.c_int, [vp, ct.POINTER(FpGraph), vp]),
     "fp_dev_levelize": (ct.c_int, [vp, ct.POINTER(FpGraph), vp, vp, vp]),
     "fp_dev_place_batch": (ct.c_int, [vp, ct.POINTER(FpBatch)]),

@@ -158,7 +158,9 @@ def stage_graph(services: list[str], flow: Flow):
             names.append(n)
         pos_to_vertex.append(vid[n])
     V = len(names)
-    has_deps = np.zeros(V, np.uint8)
+    # plain lists, one array conversion each at the end: a fleet.kdl stage has a handful of services,
+    # where per-element numpy indexing costs more than the graph (config 1 is timed per plan)
+    has_deps = bytearray(V)
     edges = []
     for v, n in enumerate(names):
         svc = flow.services.get(n)
@@ -166,18 +168,21 @@ def stage_graph(services: list[str], flow: Flow):
             continue
         has_deps[v] = 1
         for d in svc.depends_on:
-            if d in vid:
-                edges.append((vid[d], v))
-    row_ptr = np.zeros(V + 1, np.uint32)
+            u = vid.get(d)
+            if u is not None:
+                edges.append((u, v))
+    row_ptr = [0] * (V + 1)
     for d, _ in edges:
         row_ptr[d + 1] += 1
-    row_ptr = np.cumsum(row_ptr, dtype=np.uint64).astype(np.uint32)
-    col = np.zeros(len(edges), np.uint32)
-    fill = row_ptr[:-1].copy()
+    for i in range(V):
+        row_ptr[i + 1] += row_ptr[i]
+    col = [0] * len(edges)
+    fill = row_ptr[:-1]
     for d, v in edges:
         col[fill[d]] = v
         fill[d] += 1
-    return names, np.array(pos_to_vertex, np.uint32), row_ptr, col, has_deps
+    return (names, np.array(pos_to_vertex, np.uint32), np.array(row_ptr, np.uint32), np.array(col, np.uint32),
+            np.frombuffer(has_deps, np.uint8))
 
 
 def levelize_stage(services: list[str], flow: Flow, planner: Planner | None = None):
@@ -275,9 +280,9 @@ def plan_stage(flow: Flow, stage_name: str, planner: Planner | None = None,
     if len(names) == len(services):
         cont, ntab = _stage_tables(names, flow, nodes) if nodes else (None, None)
         perm, level_v, order_v, _, placed = p.plan_stage(row_ptr, col, has_deps, cont, ntab)
-        order = [services[i] for i in perm]
-        levels = [int(x) for x in level_v]
-        level_order = [services[i] for i in order_v]
+        order = [services[i] for i in perm.tolist()]
+        levels = level_v.tolist()
+        level_order = [services[i] for i in order_v.tolist()]
     else:
         order = order_by_dependencies(services, flow, p)
         levels, level_order = levelize_stage(services, flow, p)

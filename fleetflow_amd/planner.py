@@ -148,15 +148,13 @@ class Planner:
         nodes_after)."""
         rp, cl, hd = _u32(row_ptr), _u32(col), _u8(has_deps)
         V = hd.size
-        perm = np.empty(V, np.uint32)
-        level = np.empty(V, np.uint32)
-        order = np.empty(V, np.uint32)
+        out = np.empty(3 * V, np.uint32)  # perm, level, order: one allocation, passed as addresses
+        perm, level, order = out[:V], out[V:2 * V], out[2 * V:]
+        o = out.ctypes.data
         ncyc = ct.c_uint32()
-        g = FpGraph(V, cl.size, _ptr(rp), _ptr(cl) if cl.size else None, _ptr(hd))
-        u32 = _lib.u32p
+        g = FpGraph(V, cl.size, rp.ctypes.data, cl.ctypes.data if cl.size else None, hd.ctypes.data)
         if nodes is None:
-            check(self._L.fp_plan_stage(self._ctx, ct.byref(g), None, None, perm.ctypes.data_as(u32),
-                                        level.ctypes.data_as(u32), order.ctypes.data_as(u32), ct.byref(ncyc),
+            check(self._L.fp_plan_stage(self._ctx, ct.byref(g), None, None, o, o + 4 * V, o + 8 * V, ct.byref(ncyc),
                                         None, None, None, None), "fp_plan_stage")
             return perm, level, order, ncyc.value, None
         cpu, mem, req, conf = (_u32(x) for x in cont)
@@ -168,10 +166,9 @@ class Planner:
         reason = np.empty(V, np.uint8)
         cs = FpContainers(V, _ptr(cpu), _ptr(mem), _ptr(req), _ptr(conf))
         ns = FpNodes(cf.size, _ptr(cf), _ptr(mf), _ptr(lab), _ptr(cu), _ptr(sched))
-        check(self._L.fp_plan_stage(self._ctx, ct.byref(g), ct.byref(cs), ct.byref(ns), perm.ctypes.data_as(u32),
-                                    level.ctypes.data_as(u32), order.ctypes.data_as(u32), ct.byref(ncyc),
-                                    first.ctypes.data_as(u32), count.ctypes.data_as(u32), assign.ctypes.data_as(u32),
-                                    reason.ctypes.data_as(_lib.u8p)), "fp_plan_stage")
+        check(self._L.fp_plan_stage(self._ctx, ct.byref(g), ct.byref(cs), ct.byref(ns), o, o + 4 * V, o + 8 * V,
+                                    ct.byref(ncyc), first.ctypes.data, count.ctypes.data, assign.ctypes.data,
+                                    reason.ctypes.data), "fp_plan_stage")
         return perm, level, order, ncyc.value, (first, count, assign, reason, (cf, mf, lab, cu, sched))
 
     def place(self, cont, nodes, level=None):
