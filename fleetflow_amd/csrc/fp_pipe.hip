@@ -412,7 +412,7 @@ constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
 #ifndef FPP_BIG_S
 #define FPP_BIG_S 4096
 #endif
-constexpr uint32_t WIDE12_BIG_WAVES = FPP_BIG_WAVES, WIDE12_BIG_S = FPP_BIG_S;
+[[maybe_unused]] constexpr uint32_t WIDE12_BIG_WAVES = FPP_BIG_WAVES, WIDE12_BIG_S = FPP_BIG_S;
 // Batch prescan: a group with an empty batch corner skips its bucket-mask loads in the wide stages
 // (config-4 FFD 17.38 -> 15.72 ms: a batch that passes a segment mostly has every corner empty);
 // the narrow stages keep the branch-free form (config 3: 64.3 vs 65.3 ms with the skip; r03z A/B,
@@ -1352,6 +1352,7 @@ static int launch_g(hipStream_t st, unsigned grid, unsigned block, size_t lds, c
 
 typedef int (*launch_fn)(hipStream_t, unsigned, unsigned, size_t, const PipeArgs &);
 // the kernels themselves (occupancy queries)
+#ifndef FPP_BIG_TU  // (fp_pipe_big.hip compiles only the 4096-scenario kernel, below)
 static const void *const kKernel[MAX_G + 1] = {
     nullptr, (const void *)k_ffd_pipe<1, 1024>, (const void *)k_ffd_pipe<2, 1024>, (const void *)k_ffd_pipe<3, 1024>,
     (const void *)k_ffd_pipe<4, 1024>, (const void *)k_ffd_pipe<5, 1024>, (const void *)k_ffd_pipe<6, 1024>,
@@ -1376,11 +1377,38 @@ static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {
     (const void *)k_ffd_pipe<36, 64>, (const void *)k_ffd_pipe<40, 64>};
 static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G >= 12; }
 // the six-wave 12-group instantiation (WIDE12_BIG_S)
+#ifdef FPP_SPLIT_BIG
+// the 4096-scenario kernel (one-wave 12-group segments at six waves per SIMD) is compiled in its own
+// translation unit, fp_pipe_big.hip, under LLVM's iterative-ILP machine scheduler: config-4 FFD
+// 13.71 -> 13.58 ms with the same plans; the same scheduler on every kernel of this file cost
+// config 3 +0.7 % (profiles/r06o_sched_ab.txt)
+}  // namespace fpp
+int fpp_launch_wide12_big(hipStream_t st, unsigned grid, unsigned block, size_t lds, const void *args);
+const void *fpp_kernel_wide12_big();
+namespace fpp {
+static int launch_wide12_big(hipStream_t st, unsigned grid, unsigned block, size_t lds, const PipeArgs &a) {
+    return ::fpp_launch_wide12_big(st, grid, block, lds, &a);
+}
+static const launch_fn kLaunchWide12Big = launch_wide12_big;
+#define kKernelWide12Big (::fpp_kernel_wide12_big())
+#else
 static const launch_fn kLaunchWide12Big = launch_g<12, 64, WIDE12_BIG_WAVES>;
 static const void *const kKernelWide12Big = (const void *)k_ffd_pipe<12, 64, WIDE12_BIG_WAVES>;
+#endif
 static inline bool wide12_big(uint32_t S, uint32_t W, uint32_t G) { return W == 1 && G == 12 && S >= WIDE12_BIG_S; }
+#endif  // FPP_BIG_TU
 
 }  // namespace fpp
+
+#ifdef FPP_BIG_TU
+// the one kernel and its launcher (this translation unit's namespace is renamed, fp_pipe_big.hip)
+int fpp_launch_wide12_big(hipStream_t st, unsigned grid, unsigned block, size_t lds, const void *args) {
+    return fpp::launch_g<12, 64, fpp::WIDE12_BIG_WAVES>(st, grid, block, lds, *static_cast<const fpp::PipeArgs *>(args));
+}
+const void *fpp_kernel_wide12_big() { return (const void *)fpp::k_ffd_pipe<12, 64, fpp::WIDE12_BIG_WAVES>; }
+#endif
+
+#ifndef FPP_BIG_TU
 
 using namespace fpp;
 
@@ -1791,3 +1819,4 @@ extern "C" int fp_debug_pipe_stats(unsigned long long *out, int reset) {
     return FP_OK;
 }
 #endif
+#endif  // !FPP_BIG_TU
