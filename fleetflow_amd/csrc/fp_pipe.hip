@@ -1379,9 +1379,9 @@ static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G >= 12; }
 // the six-wave 12-group instantiation (WIDE12_BIG_S)
 #ifdef FPP_SPLIT_BIG
 // the 4096-scenario kernel (one-wave 12-group segments at six waves per SIMD) is compiled in its own
-// translation unit, fp_pipe_big.hip, under LLVM's iterative-ILP machine scheduler: config-4 FFD
-// 13.71 -> 13.58 ms with the same plans; the same scheduler on every kernel of this file cost
-// config 3 +0.7 % (profiles/r06o_sched_ab.txt)
+// translation unit, fp_pipe_big.hip, under LLVM's iterative max-occupancy machine scheduler:
+// config-4 FFD 13.56 (iterative-ILP; 13.69 default) -> 13.21 ms with the same plans; on the rest of
+// this file no strategy beat the default beyond noise (profiles/r06o_sched_ab.txt)
 }  // namespace fpp
 int fpp_launch_wide12_big(hipStream_t st, unsigned grid, unsigned block, size_t lds, const void *args);
 const void *fpp_kernel_wide12_big();
