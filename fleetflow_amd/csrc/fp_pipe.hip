@@ -953,8 +953,9 @@ k_ffd_pipe(const PipeArgs a_arg) {
     }
     if (G == 1) {
         // one-group stages: the systolic fill does not track the nodes it placed on; a placement of a
-        // container with any nonzero field changes its node's record (capacity only shrinks, and a
-        // conflict bit must be new to fit), and all-zero containers set usedbits above
+        // container with nonzero cpu, mem or conf changes its node's record (capacity only shrinks,
+        // and a conflict bit must be new to fit); all-zero containers set usedbits above and
+        // label-only ones (only req nonzero) are marked by fpp_group_sys
         const uint32_t n = gbase * 64 + lane;
         if (n < N && (schedbits & 1u) &&
             (a.cf[nb + n] != rcf[0] || a.mf[nb + n] != rmf[0] || a.cu[nb + n] != rcu[0]))
@@ -1523,17 +1524,19 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     g->R = R;
     g->lds = lds_bytes(W, G, R);
     // resident segments on this device (0 if unknown)
-    uint64_t slots_total = 0;
-    {
+    // (the kernel fp_pipe_launch will run: the six-wave one only with unbounded links)
+    auto resident_of = [&](bool big) -> uint64_t {
         int dev_cu = 0, occ = 0;
         (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
         const bool wide = wide_g(W, G);
-        const void *fn = wide12_big(S, W, G) ? kKernelWide12Big
+        const void *fn = big ? kKernelWide12Big
                          : wide ? (G / 4 < sizeof(kKernelWide) / sizeof(kKernelWide[0]) ? kKernelWide[G / 4] : nullptr)
                                 : (G < sizeof(kKernel) / sizeof(kKernel[0]) ? kKernel[G] : nullptr);
         if (fn && dev_cu > 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), g->lds) == hipSuccess && occ > 0)
-            slots_total = (uint64_t)occ * (uint64_t)dev_cu;
-    }
+            return (uint64_t)occ * (uint64_t)dev_cu;
+        return 0;
+    };
+    uint64_t slots_total = resident_of(wide12_big(S, W, G));
     g->resident = (uint32_t)(slots_total < 0xFFFFFFFFull ? slots_total : 0xFFFFFFFFull);
     const bool fits = B > 1 && slots_total && (uint64_t)S * B <= slots_total;
     // segment lag (kernel comment).  Measured FFD kernel ms (7 segments of 12 groups, 4096
@@ -1566,6 +1569,13 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     g->bounded = (uint32_t)fp_opt(c, FP_OPT_LINK_BOUNDED, (fits && margin && g->lag == 0 && ring < full) ? 1 : 0);
     if (B <= 1) g->bounded = 0;
     g->slots = g->bounded ? (ring < full ? ring : full) : full;
+    if (g->bounded && wide12_big(S, W, G)) {
+        // a bounded ring runs the five-wave 12-group kernel (fp_pipe_launch), which holds fewer
+        // segments: report (FP_GEOM_RESIDENT) and size against that one.  The automatic
+        // choice never bounds such a batch (S * B exceeds either kernel's slots), only a forced one
+        const uint64_t r5 = resident_of(false);
+        g->resident = (uint32_t)(r5 < 0xFFFFFFFFull ? r5 : 0xFFFFFFFFull);
+    }
     // systolic group fill (fp_pipe_sys.h): queues of at least this many containers (compiled for
     // stages of at most SYS_MAX_G groups)
     // Default: queues of >= 32 containers in the narrow stages (configs 2 / 3 / 5: one scenario,

@@ -260,6 +260,17 @@ __device__ __forceinline__ void fpp_group_sys(uint64_t q, uint64_t &placed, uint
     const uint32_t lane = __lane_id();
     const bool inq = (q >> lane) & 1ull;
     const uint64_t hit = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu);
+    if (G == 1 && (extra & 0xC000u) == 0x4000u) {
+        // the DPP-folded fill of a one-group stage leaves `touched` alone and k_ffd_pipe counts the
+        // nodes whose records changed; a label-only container (cpu = mem = conf = 0, req != 0)
+        // changes none, so its node is marked here (n_nodes_used undercounted)
+        uint64_t lo = __builtin_amdgcn_ballot_w64(inq && asg != 0xFFFFFFFFu && (cpu | mem | conf) == 0u);
+        while (lo) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(lo);
+            lo &= lo - 1;
+            touched |= 1ull << ((__builtin_amdgcn_readlane(asg, l) - gbg) & 63u);
+        }
+    }
 #ifdef FP_PIPE_STATS
     nhit += (uint32_t)__builtin_popcountll(hit);
 #else

@@ -285,7 +285,12 @@ extern "C" int fp_plan_stage(fp_ctx *c, const fp_graph *g, const fp_containers *
     const size_t o_cf = take((size_t)N * 4), o_mf = take((size_t)N * 4), o_cu = take((size_t)N * 4);
     const size_t bytes = off * 4;
     if (bytes > c->h_map_cap) {
-        if (c->h_map) (void)hipHostFree(c->h_map);
+        // the previous plan's kernel may still be retiring (the host returned once its completion
+        // word was set): let it finish before its mapped buffer goes
+        if (c->h_map) {
+            FP_HIP(hipStreamSynchronize(c->stream));
+            (void)hipHostFree(c->h_map);
+        }
         c->h_map = nullptr;
         c->d_map = nullptr;
         c->h_map_cap = 0;

@@ -121,6 +121,13 @@ class Planner:
         return ms.value, n.value
 
     # -- host-pointer API ------------------------------------------------------------
+    # Every array is read (or written) for the length the call's sizes imply, so a shorter one would be
+    # read out of bounds by the library: refused with ValueError first, as lib.rs returns FP_EINVAL.
+    @staticmethod
+    def _need(cond, what):
+        if not cond:
+            raise ValueError(what)
+
     def legacy_order(self, has_deps):
         """engine.rs:67-85 on indices: has_deps[i] = known && depends_on non-empty."""
         hd = _u8(has_deps)
@@ -132,6 +139,7 @@ class Planner:
     def levelize(self, row_ptr, col, has_deps):
         rp, cl, hd = _u32(row_ptr), _u32(col), _u8(has_deps)
         V = hd.size
+        self._need(V == 0 or rp.size == V + 1, "row_ptr must hold V + 1 entries")
         level = np.empty(V, np.uint32)
         order = np.empty(V, np.uint32)
         ncyc = ct.c_uint32()
@@ -148,6 +156,7 @@ class Planner:
         nodes_after)."""
         rp, cl, hd = _u32(row_ptr), _u32(col), _u8(has_deps)
         V = hd.size
+        self._need(V == 0 or rp.size == V + 1, "row_ptr must hold V + 1 entries")
         out = np.empty(3 * V, np.uint32)  # perm, level, order: one allocation, passed as addresses
         perm, level, order = out[:V], out[V:2 * V], out[2 * V:]
         o = out.ctypes.data
@@ -160,6 +169,8 @@ class Planner:
         cpu, mem, req, conf = (_u32(x) for x in cont)
         cf, mf = _u32(nodes[0]).copy(), _u32(nodes[1]).copy()
         lab, cu, sched = _u32(nodes[2]), _u32(nodes[3]).copy(), _u8(nodes[4])
+        self._need(all(x.size == V for x in (cpu, mem, req, conf)), "every container array must hold V entries")
+        self._need(all(x.size == cf.size for x in (mf, lab, cu, sched)), "every node array must hold N entries")
         first = np.empty(V, np.uint32)
         count = np.empty(V, np.uint32)
         assign = np.empty(V, np.uint32)
@@ -179,9 +190,12 @@ class Planner:
         cf, mf = _u32(nodes[0]).copy(), _u32(nodes[1]).copy()
         lab, cu, sched = _u32(nodes[2]), _u32(nodes[3]).copy(), _u8(nodes[4])
         C, N = cpu.size, cf.size
+        lv = _u32(level) if level is not None else None
+        self._need(all(x.size == C for x in (mem, req, conf)), "every container array must hold C entries")
+        self._need(all(x.size == N for x in (mf, lab, cu, sched)), "every node array must hold N entries")
+        self._need(lv is None or lv.size == C, "level must hold C entries")
         assign = np.empty(C, np.uint32)
         reason = np.empty(C, np.uint8)
-        lv = _u32(level) if level is not None else None
         cs = FpContainers(C, _ptr(cpu), _ptr(mem), _ptr(req), _ptr(conf))
         ns = FpNodes(N, _ptr(cf), _ptr(mf), _ptr(lab), _ptr(cu), _ptr(sched))
         check(self._L.fp_place(self._ctx, ct.byref(cs), ct.byref(ns),
@@ -195,8 +209,10 @@ class Planner:
         cpu, mem, req, conf = (_u32(x) for x in cont)
         cf, mf = _u32(nodes[0]).copy(), _u32(nodes[1]).copy()
         lab, cu, sched = _u32(nodes[2]), _u32(nodes[3]).copy(), _u8(nodes[4])
-        assert cpu.size == S * C and cf.size == S * N
         lv = _u32(level) if level is not None else None
+        self._need(all(x.size == S * C for x in (cpu, mem, req, conf)), "every container array must hold S * C entries")
+        self._need(all(x.size == S * N for x in (cf, mf, lab, cu, sched)), "every node array must hold S * N entries")
+        self._need(lv is None or lv.size == S * C, "level must hold S * C entries")
         assign = np.empty(S * C, np.uint32)
         reason = np.empty(S * C, np.uint8)
         cost = np.empty(S, np.uint64)

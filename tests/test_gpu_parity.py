@@ -656,6 +656,56 @@ def test_ffd_zero_demand_mixed(N, planner, O, geometry):
     _check_ffd(planner, O, (cpu[:300], mem[:300], req[:300], conf[:300]), (cf, mf, lab, cu, np.zeros(N, np.uint8)))
 
 
+@pytest.mark.parametrize("n_lab", [32, 64, 100])
+@pytest.mark.parametrize("N", [5, 64])
+def test_label_only_containers_count_their_node(n_lab, N, planner, O):
+    """a one-group stage's systolic fill counts the nodes whose records changed,
+    and a label-only container (cpu = mem = conf = 0, req != 0) changes none.  Here >= 32 of them
+    (a systolic queue) fit only node 3, which nothing else uses: the packed cost must count node 3
+    (n_nodes_used, SPEC.md 2.4) exactly as the oracle does.  Also the serial loop (threshold 64)."""
+    S, base, k = 3, 11, 20
+    conts, nodes = [], []
+    for s in range(S):
+        cpu = [5 + s] * k + [0] * n_lab
+        mem = [7] * k + [0] * n_lab
+        req = [0] * k + [1 << 4] * n_lab
+        conf = [0] * (k + n_lab)
+        conts.append(tuple(np.array(x, np.uint32) for x in (cpu, mem, req, conf)))
+        lab = np.zeros(N, np.uint32)
+        lab[3] = 1 << 4
+        nodes.append((np.full(N, 1000, np.uint32), np.full(N, 1000, np.uint32), lab, np.zeros(N, np.uint32),
+                       np.ones(N, np.uint8)))
+    C = k + n_lab
+    cat = lambda parts, i: np.concatenate([p[i] for p in parts])  # noqa: E731
+    for sys_thr in (None, 64):
+        planner.set_option("systolic", sys_thr if sys_thr is not None else -1)  # -1: FP_OPT_AUTO
+        try:
+            assign, reason, cost, _ = planner.place_batch(S, C, N, [cat(conts, i) for i in range(4)],
+                                                          [cat(nodes, i) for i in range(5)], scen_base=base)
+        finally:
+            planner.set_option("systolic")
+        for s in range(S):
+            ea, er, _, _ = O.place(conts[s], nodes[s])
+            assert np.array_equal(assign[s * C:(s + 1) * C], ea)
+            assert np.array_equal(reason[s * C:(s + 1) * C], er)
+            assert int(cost[s]) == O.cost(ea, N, base + s), (s, sys_thr)
+            assert 3 in set(ea.tolist())
+
+
+def test_forced_bounded_geometry_reports_the_launched_kernel(planner, opts):
+    """a 4096-scenario batch runs the six-wave kernel only with unbounded links; a
+    forced bounded ring runs the five-wave one, and fp_place_geometry's resident slots must be that
+    kernel's (the same 12-group one-wave kernel a 2048-scenario batch runs)."""
+    auto = planner.geometry(4096, 50_000, 5_000)
+    five = planner.geometry(2048, 50_000, 5_000)
+    assert auto["groups"] == five["groups"] == 12 and auto["stages"] == five["stages"] == 1
+    assert not auto["bounded"]
+    opts(link_bounded=1)
+    forced = planner.geometry(4096, 50_000, 5_000)
+    assert forced["bounded"] == 1
+    assert forced["resident"] == five["resident"] < auto["resident"]
+
+
 @pytest.mark.parametrize("S,C,N", [(3, 700, 300), (5, 3000, 5000), (4, 50_000, 5_000)])
 def test_feasibility_batch_vs_oracle(S, C, N, planner, O):
     """Stage 2 batched over scenarios (fp_dev_feasibility_batch): every scenario's first

@@ -111,12 +111,40 @@ def test_constants_match():
     assert "pub const FP_OPT_AUTO: i64 = -1;" in rs
 
 
-def test_build_script_compiles_every_library_source():
+def _make_dry_run(*args):
+    """The commands `make -B -n` would run in fleetflow_amd/csrc (nothing is built)."""
+    import subprocess
+    csrc = os.path.join(ROOT, "fleetflow_amd", "csrc")
+    r = subprocess.run(["make", "-B", "-n", "-C", csrc, *args], capture_output=True, text=True, check=True)
+    return [ln.strip() for ln in r.stdout.splitlines() if ln.strip() and not ln.startswith("make")]
+
+
+def test_build_script_runs_the_makefile_recipe():
+    """build.rs has no compiler command line of its own: it runs fleetflow_amd/csrc/Makefile with the
+    objects and the library under cargo's OUT_DIR (a second copy of the recipe
+    had drifted -- no -DFPP_SPLIT_BIG, no fp_pipe_big.hip under its own machine scheduler).  The
+    Makefile's dry run with those two variables must be the in-tree recipe command for command
+    (every translation unit with its own flags, the same link line) once the paths are mapped."""
+    br = open(os.path.join(ROOT, "integration", "fleetflow-placement", "build.rs")).read()
+    code = re.sub(r"//[^\n]*", "", br)
+    assert 'Command::new("make")' in code
+    assert '"BUILD={}"' in code and '"OUT={}"' in code and "arg(&src)" in code
+    assert "offload-arch" not in code and ".hip" not in code  # no recipe of its own
+    assert "rerun-if-changed={}\", src.display()" in code  # the whole source directory
+    base = _make_dry_run()
+    alt = _make_dry_run("BUILD=/cargo/out/obj", "OUT=/cargo/out/libfleetplace.so")
+    mapped = [c.replace("/cargo/out/obj", "build").replace("/cargo/out/libfleetplace.so", "../libfleetplace.so")
+              for c in alt]
+    assert mapped == base
+    compiles = [c for c in base if " -c " in c]
     mk = open(os.path.join(ROOT, "fleetflow_amd", "csrc", "Makefile")).read()
     srcs = re.search(r"SRCS := (.*)", mk).group(1).split()
-    br = open(os.path.join(ROOT, "integration", "fleetflow-placement", "build.rs")).read()
-    listed = re.findall(r'"(fp_\w+\.hip)"', br)
-    assert sorted(listed) == sorted(srcs)
+    assert sorted(re.search(r" -c (\S+\.hip)", c).group(1) for c in compiles) == sorted(srcs + ["fp_pipe_big.hip"])
+    flags = {re.search(r" -c (\S+\.hip)", c).group(1): c for c in compiles}
+    assert "-DFPP_SPLIT_BIG" in flags["fp_pipe.hip"]
+    assert "--amdgpu-sched-strategy=" in flags["fp_pipe_big.hip"]
+    link = [c for c in base if " -shared " in c and "../libfleetplace.so" in c]
+    assert len(link) == 1 and all(f"build/{s[:-4]}.o" in link[0] for s in srcs + ["fp_pipe_big.hip"])
 
 
 def _calls(src, prefix="ffi::"):
