@@ -25,7 +25,7 @@ OPTIONS = {"pipe_w": 0, "pipe_seg": 1, "pipe_r": 2, "pipe_lag": 3, "link_slots":
            "pipe_flush": 6, "spin_ticks": 7, "kpack": 8, "scen_sort": 9, "segsort": 10, "systolic": 11,
            "levelize_sync": 12, "systolic_extra": 13, "screen": 14, "payload_lds": 15, "systolic_valu": 16, "link_publish": 17,
            "level_sort": 18, "level_small": 19, "pipe_prio": 20,
-           "indeg_bin": 21}
+           "indeg_bin": 21, "packed": 22}
 # fp_place_geometry out[] (fleetplace.h FP_GEOM_*)
 GEOM_FIELDS = ("groups", "stages", "segments", "ring", "lag", "link_slots", "bounded", "resident", "systolic")
 
@@ -77,6 +77,7 @@ SIGNATURES = {
     "fp_abi_version": (ct.c_int, []),
     "fp_ctx_profile": (ct.c_int, [vp, ct.c_int]),
     "fp_ctx_kernel_stats": (ct.c_int, [vp, ct.c_int, ct.POINTER(ct.c_double), ct.POINTER(ct.c_uint64)]),
+    "fp_ctx_place_path": (ct.c_int, [vp, u32p]),
     "fp_ctx_set_option": (ct.c_int, [vp, ct.c_int, ct.c_int64]),
     "fp_ctx_get_option": (ct.c_int, [vp, ct.c_int, ct.POINTER(ct.c_int64)]),
     "fp_legacy_order": (ct.c_int, [vp, ct.POINTER(FpGraph), u32p]),

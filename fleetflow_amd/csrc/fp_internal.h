@@ -58,6 +58,9 @@ struct fp_ctx {
     // the asynchronous levelizer's work queues (fp_order.hip), kept between calls: a clean finish
     // leaves them empty, and the flag in their last 256 bytes tells the next call whether to refill
     void *lvl_q = nullptr;
+    // the last placement's range words (CN_ORC.. of its workspace: OR cpu, OR mem, kernel path),
+    // read by fp_ctx_place_path
+    uint32_t *last_rng = nullptr;
     size_t lvl_q_cap = 0;
     // profiling
     bool profile = false;
@@ -155,10 +158,12 @@ uint32_t fp_pipe_kpack(const fp_ctx *c, uint32_t C);
 // ready: the per-scenario LDS sort already wrote order, s_cpu, s_mem and s_idx (only the
 // req / conf / CYCLE gather remains); null: gather everything from order + sorted keys.
 // thr: the pipeline's bucket thresholds in device memory ([FP_BUCKETS] cpu, then mem)
+// rng: [2] the OR of every container cpu / mem value of the batch (the sort kernels wrote it); the
+// pipeline adds the nodes' and runs the packed kernel when the values pack (null: u32 kernels only)
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
                    const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *thr,
-                   const fp_pipe_soa *ready);
+                   const fp_pipe_soa *ready, uint32_t *rng);
 
 // ---- device helpers ----
 namespace fpd {

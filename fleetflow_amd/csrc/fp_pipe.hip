@@ -28,6 +28,8 @@
 // history; DESIGN.md 7 keeps their numbers.)
 #include "fp_pipe_asm.h"
 #include "fp_pipe_sys.h"
+#include "fp_pipe_pk.h"
+#include "fp_pipe_tus.h"
 #include <stdlib.h>
 #include <string.h>
 #include <mutex>
@@ -128,6 +130,12 @@ struct PipeArgs {
     uint64_t spin_ticks;    // deadlock guard, s_memrealtime ticks (100 MHz)
     const uint32_t *thr;    // [2K] device: ascending thresholds, cpu then mem, thr[0] = thr[K] = 0
     uint32_t prio;          // wave priority mode (FP_PRIO_LEVEL comment)
+    // packed-capacity pair (fp_pipe_pk.h): the batch's OR of every cpu value [0] and mem value [1]
+    // (containers and schedulable nodes; k_scen_sort / k_make_keys / k_node_summary), and the mode:
+    // 0 = the u32 kernel alone; 1 / 2 = the u32 / packed kernel of a pair launched back to back,
+    // each running the batch only when the values do not / do pack (the other one returns)
+    uint32_t *rng;  // [3]: [2] = the kernel that ran (1 u32, 2 packed; fp_ctx_place_path)
+    uint32_t pk_mode;
 };
 
 // Control words (heads, tails, counts, abort flags) are read by every lane at one address: the
@@ -289,29 +297,39 @@ constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
 constexpr uint32_t SYS_MAX_G = 4;
 // The serial loop over one group's queue is the exec-masked loop (fp_pipe_asm.h fpp_group_x:
 // 172 vs 264 cycles per container for round 2's readlane / writelane loop).
-template <uint32_t G, bool UPD, bool IB, uint32_t... gs, class Rec>
+template <uint32_t G, bool UPD, bool IB, bool PK, uint32_t... gs, class Rec>
 __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...>, uint32_t &nxt, uint64_t &placed,
                                            uint32_t &asg, uint32_t &used, uint32_t &used_hi, Rec &rcf, Rec &rmf,
                                            Rec &rcu, const Rec &rlab, uint32_t cpu, uint32_t mem, uint32_t req,
                                            uint32_t conf, uint32_t cand, uint32_t cand_hi, uint32_t my_t, uint32_t lane,
                                            uint64_t *Mw, uint32_t mlane, uint32_t gb64, uint32_t qc, uint32_t qm, uint32_t &nchk,
-                                           uint32_t &nhit, uint32_t sys, unsigned long long (&gst)[4]) {
+                                           uint32_t &nhit, uint32_t sys, unsigned long long (&gst)[4], uint32_t cw,
+                                           uint32_t qw, uint32_t sc_c, uint32_t sc_m) {
+    // PK (fp_pipe_pk.h): rcf[g] holds the packed (cpu, mem) record and rmf is unused; cw / qw are the
+    // container's and the batch corner's packed demands, sc_c / sc_m the batch's shifts
     constexpr uint32_t pf_max = G <= SYS_MAX_G ? PF_MAX_NARROW : PF_MAX_WIDE;
     (
         [&] {
             uint64_t q = __builtin_amdgcn_ballot_w64(nxt == gs);
             if (pf_max > 0 && q) {
-                uint64_t e = (__builtin_amdgcn_ballot_w64(rcf[gs] >= qc) & __builtin_amdgcn_ballot_w64(rmf[gs] >= qm));
+                uint64_t e;
+                if constexpr (PK) e = __builtin_amdgcn_ballot_w64(pk_fits(rcf[gs], qw));
+                else e = (__builtin_amdgcn_ballot_w64(rcf[gs] >= qc) & __builtin_amdgcn_ballot_w64(rmf[gs] >= qm));
                 if (__builtin_popcountll(e) <= pf_max) {
                     bool ok = false;
                     while (e) {
                         const uint32_t l = (uint32_t)__builtin_ctzll(e);
                         e &= e - 1;
-                        const uint32_t ncf = __builtin_amdgcn_readlane(rcf[gs], l);
-                        const uint32_t nmf = __builtin_amdgcn_readlane(rmf[gs], l);
                         const uint32_t nlb = __builtin_amdgcn_readlane(rlab[gs], l);
                         const uint32_t ncu = __builtin_amdgcn_readlane(rcu[gs], l);
-                        ok |= (ncf >= cpu) & (nmf >= mem) & (((req & nlb) | (conf & ncu)) == 0u);
+                        if constexpr (PK) {
+                            const uint32_t nw = __builtin_amdgcn_readlane(rcf[gs], l);
+                            ok |= ((((nw - cw) & PK_GUARD) | (req & nlb) | (conf & ncu)) == 0u);
+                        } else {
+                            const uint32_t ncf = __builtin_amdgcn_readlane(rcf[gs], l);
+                            const uint32_t nmf = __builtin_amdgcn_readlane(rmf[gs], l);
+                            ok |= (ncf >= cpu) & (nmf >= mem) & (((req & nlb) | (conf & ncu)) == 0u);
+                        }
                     }
                     const uint64_t fit = q & __builtin_amdgcn_ballot_w64(ok);
                     if (q != fit) {  // the others move on: next candidate group above g, or none
@@ -327,15 +345,35 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                 const unsigned long long gc0 = STAT_GCLK();
                 // long queues (a filling group): the systolic loop, else the serial one
                 // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
-                if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
-                    fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
-                                         req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm, sys >> 16);
-                else
-                    fpp_group_x<gs, G, IB>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
-                                       req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
+                if constexpr (PK) {
+                    if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
+                        fpp_group_sysp<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rcu[gs], rlab[gs], cw, req, conf,
+                                              cand, cand_hi, gb64, nchk, nhit, qw, sys >> 16);
+                    else
+                        fpp_group_xp<gs, G, IB>(q, placed, touched, asg, nxt, rcf[gs], rcu[gs], rlab[gs], cw, req, conf,
+                                                cand, cand_hi, gb64, nchk, nhit, qw);
+                } else {
+                    if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
+                        fpp_group_sys<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                                             req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm, sys >> 16);
+                    else
+                        fpp_group_x<gs, G, IB>(q, placed, touched, asg, nxt, rcf[gs], rmf[gs], rcu[gs], rlab[gs], cpu, mem,
+                                               req, conf, cand, cand_hi, gb64, nchk, nhit, qc, qm);
+                }
                 const unsigned long long gc1 = STAT_GCLK();
                 if (STAT_FINE) { gst[0] += gc1 - gc0; gst[2] += 1; gst[3] += (uint32_t)__builtin_popcountll(touched); }
                 if (touched) {
+                    // a touched node's new free capacity (unpacked in the packed kernels)
+                    auto node_cm = [&](uint32_t l, uint32_t &nc, uint32_t &nm) {
+                        if constexpr (PK) {
+                            const uint32_t nw = __builtin_amdgcn_readlane(rcf[gs], l);
+                            nc = pk_cpu(nw, sc_c);
+                            nm = pk_mem(nw, sc_m);
+                        } else {
+                            nc = __builtin_amdgcn_readlane(rcf[gs], l);
+                            nm = __builtin_amdgcn_readlane(rmf[gs], l);
+                        }
+                    };
                     if constexpr (IB) {
                         // one-wave kernels: lane selects read the masks directly (fpp_lane_sel).
                         // Bucket lane k clears node l's bit when the node's new free capacity is
@@ -350,8 +388,8 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                             while (tt) {
                                 const uint32_t l = (uint32_t)__builtin_ctzll(tt);
                                 tt &= tt - 1;
-                                const uint32_t nc = __builtin_amdgcn_readlane(rcf[gs], l);
-                                const uint32_t nm = __builtin_amdgcn_readlane(rmf[gs], l);
+                                uint32_t nc, nm;
+                                node_cm(l, nc, nm);
                                 const uint64_t below = (__builtin_amdgcn_ballot_w64(my_t > nc) & 0xFFFFFFFFull) |
                                                        (__builtin_amdgcn_ballot_w64(my_t > nm) & ~0xFFFFFFFFull);
                                 if (l < 32) clr_lo = fpp_lane_sel<true>(below, clr_lo | (1u << l), clr_lo);
@@ -373,8 +411,8 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                             while (tt) {
                                 const uint32_t l = (uint32_t)__builtin_ctzll(tt);
                                 tt &= tt - 1;
-                                const uint32_t nc = __builtin_amdgcn_readlane(rcf[gs], l);
-                                const uint32_t nm = __builtin_amdgcn_readlane(rmf[gs], l);
+                                uint32_t nc, nm;
+                                node_cm(l, nc, nm);
                                 // a bit at or below the node's new free capacity stays; every bit above
                                 // it goes (clearing a bit that was already clear is harmless, so the
                                 // capacity before the queue is not needed)
@@ -420,7 +458,7 @@ constexpr uint32_t WIDE_WAVES = 3, WIDE12_WAVES = 5;
 // FFD 15.62 -> 15.06 ms, config 3 64.3 -> 63.6 ms; r03aa/r03ab).  Measured slower and removed in
 // round 4: per-group capacity bounds in place of the corner ballots (15.73 vs 15.08
 // ms, r03af), req / conf of link input loaded after the prescan (15.45 vs 15.08 ms, r03ac).
-template <uint32_t G, uint32_t BLK, uint32_t WV = 0>
+template <uint32_t G, uint32_t BLK, uint32_t WV = 0, bool PK = false>
 __global__ __launch_bounds__(BLK, BLK == 64 ? (WV ? WV : G == 12 ? WIDE12_WAVES : WIDE_WAVES) : 1) void
 k_ffd_pipe(const PipeArgs a_arg) {
     // the arguments are read through the kernarg segment (memory), not promoted to SGPRs for the
@@ -452,6 +490,16 @@ k_ffd_pipe(const PipeArgs a_arg) {
     uint32_t *CNT = CTL + (W - 1) * 8;
     uint32_t *D = CNT + 8;
 
+    // the packed pair: this kernel runs the batch only if its values pack (PK) / do not (!PK)
+    uint32_t sc_c = 0, sc_m = 0;
+    if (PK || a.pk_mode) {
+        const uint32_t orc = __builtin_amdgcn_readfirstlane(a.rng[0]), orm = __builtin_amdgcn_readfirstlane(a.rng[1]);
+        sc_c = orc ? (uint32_t)__builtin_ctz(orc) : 0u;
+        sc_m = orm ? (uint32_t)__builtin_ctz(orm) : 0u;
+        const bool packs = (orc >> sc_c) <= PK_FIELD_MAX && (orm >> sc_m) <= PK_FIELD_MAX;
+        if (packs != PK) return;  // uniform: the other kernel of the pair takes the batch
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.rng) a.rng[2] = PK ? 2u : 1u;  // fp_ctx_place_path
     for (uint32_t i = threadIdx.x; i < (W - 1) * 8 + 8; i += blockDim.x) CTL[i] = 0;
     __syncthreads();
     // Ticket order = start order.  Ticket t is round r = t / B, segment b = t % B, and
@@ -511,8 +559,12 @@ k_ffd_pipe(const PipeArgs a_arg) {
             const int o = in ? (int)(g * 64) : -(int)n0;  // padding lanes read node 0 of the scenario
             const bool sc = in && sc0[o] != 0;
             const uint32_t x = cf0[o], y = mf0[o], z = cu0[o], l = lb0[o];
-            rcf[g] = sc ? x : 0u;
-            rmf[g] = sc ? y : 0u;
+            if constexpr (PK) {
+                rcf[g] = sc ? pk_pack(x, y, sc_c, sc_m) : 0u;  // rmf unused
+            } else {
+                rcf[g] = sc ? x : 0u;
+                rmf[g] = sc ? y : 0u;
+            }
             rcu[g] = sc ? z : 0xFFFFFFFFu;
             rlab[g] = sc ? ~l : 0xFFFFFFFFu;
             schedbits |= sc ? (GM(1) << g) : GM(0);
@@ -535,8 +587,9 @@ k_ffd_pipe(const PipeArgs a_arg) {
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {  // every lane takes part in each ballot
             const bool sc = (schedbits >> g) & 1u;
-            const uint64_t bc = __builtin_amdgcn_ballot_w64(sc & (rcf[g] >= tc));
-            const uint64_t bm = __builtin_amdgcn_ballot_w64(sc & (rmf[g] >= tm));
+            const uint32_t ncf = PK ? pk_cpu(rcf[g], sc_c) : rcf[g], nmf = PK ? pk_mem(rcf[g], sc_m) : rmf[g];
+            const uint64_t bc = __builtin_amdgcn_ballot_w64(sc & (ncf >= tc));
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(sc & (nmf >= tm));
             if (lane == k) {
                 Mw[((size_t)g * K + k) * 2] = bc;
                 Mw[((size_t)g * K + k) * 2 + 1] = bm;
@@ -729,13 +782,17 @@ k_ffd_pipe(const PipeArgs a_arg) {
         const uint64_t vm = __builtin_amdgcn_ballot_w64(valid);
         const uint32_t qc = vm ? __builtin_amdgcn_readlane(cpu, 63 - __builtin_clzll(vm)) : 0xFFFFFFFFu;
         const uint32_t qm = wave_min(valid ? mem : 0xFFFFFFFFu);
+        // packed demands (this batch's values are multiples of the shifts: exact)
+        const uint32_t cw = PK ? pk_pack(cpu, mem, sc_c, sc_m) : 0u;
+        const uint32_t qw = PK ? pk_pack(qc, qm, sc_c, sc_m) : 0u;
         // every mask load is issued before the first use (no per-group LDS round trip)
         const uint32_t oc = kc * 2, om = km * 2 + 1;
         constexpr bool prescan_skip = G > SYS_MAX_G;
         GM cand = 0;
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
-            const uint64_t e = (__builtin_amdgcn_ballot_w64(rcf[g] >= qc) & __builtin_amdgcn_ballot_w64(rmf[g] >= qm));
+            const uint64_t e = PK ? __builtin_amdgcn_ballot_w64(pk_fits(rcf[g], qw))
+                                  : (__builtin_amdgcn_ballot_w64(rcf[g] >= qc) & __builtin_amdgcn_ballot_w64(rmf[g] >= qm));
             const uint64_t *mg = Mw + (size_t)g * K * 2;
             if (prescan_skip) {
                 // a group whose corner is empty fits no container of the batch: no mask loads
@@ -780,10 +837,11 @@ k_ffd_pipe(const PipeArgs a_arg) {
             unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
             if (prio == 1u && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
             if (todo)
-                fpp_groups<G, (G > 1), (BLK == 64 || (FPP_IB1024 && G > SYS_MAX_G)) && FPP_IB>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+                fpp_groups<G, (G > 1), (BLK == 64 || (FPP_IB1024 && G > SYS_MAX_G)) && FPP_IB, PK>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw, mlane,
-                                       __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst);
+                                       __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst,
+                                       cw, qw, sc_c, sc_m);
             if (prio == 1u && todo) __builtin_amdgcn_s_setprio(0);
             if (STAT_ON) { st_checks += nchk; st_hits += nhit; }
             if (STAT_FINE) { ck_gx += gst[0]; ck_gu += gst[1]; st_queues += (uint32_t)gst[2]; st_touched += (uint32_t)gst[3]; }
@@ -958,7 +1016,9 @@ k_ffd_pipe(const PipeArgs a_arg) {
         // label-only ones (only req nonzero) are marked by fpp_group_sys
         const uint32_t n = gbase * 64 + lane;
         if (n < N && (schedbits & 1u) &&
-            (a.cf[nb + n] != rcf[0] || a.mf[nb + n] != rmf[0] || a.cu[nb + n] != rcu[0]))
+            ((PK ? (a.cf[nb + n] != pk_cpu(rcf[0], sc_c) || a.mf[nb + n] != pk_mem(rcf[0], sc_m))
+                 : (a.cf[nb + n] != rcf[0] || a.mf[nb + n] != rmf[0])) ||
+             a.cu[nb + n] != rcu[0]))
             usedbits |= 1u;
     }
     {  // nodes of this stage that received a container
@@ -989,8 +1049,8 @@ k_ffd_pipe(const PipeArgs a_arg) {
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t n = (gbase + g) * 64 + lane;
         if (n < N && ((schedbits >> g) & 1u)) {  // unschedulable records were never loaded
-            a.cf[nb + n] = rcf[g];
-            a.mf[nb + n] = rmf[g];
+            a.cf[nb + n] = PK ? pk_cpu(rcf[g], sc_c) : rcf[g];
+            a.mf[nb + n] = PK ? pk_mem(rcf[g], sc_m) : rmf[g];
             a.cu[nb + n] = rcu[g];
         }
     }
@@ -1030,44 +1090,69 @@ __global__ void k_cost_reduce(uint32_t S, uint32_t B, uint32_t scen_base, const 
 // NOFIT without entering the pipeline, exactly as the sequential first fit would reject it at
 // the last node.  In the synthetic configs 3 and 4 that is every container requiring one of the
 // 19 label bits no node carries (~18 %): each of them used to walk every segment.
-__global__ __launch_bounds__(256) void k_node_summary(uint32_t N, const uint32_t *__restrict__ lab,
+// RANGE: the same pass also ORs the schedulable nodes' free cpu / mem into rng[0] / rng[1] (the
+// packed-capacity decision, fp_pipe_pk.h; one atomic per block and word).  !SUMM: that alone.
+template <bool SUMM, bool RANGE>
+__global__ __launch_bounds__(256) void k_node_summary(uint32_t N, const uint32_t *__restrict__ cf,
+                                                      const uint32_t *__restrict__ mf, const uint32_t *__restrict__ lab,
                                                       const uint32_t *__restrict__ cu,
-                                                      const uint8_t *__restrict__ sched, uint32_t *__restrict__ summ) {
+                                                      const uint8_t *__restrict__ sched, uint32_t *__restrict__ summ,
+                                                      uint32_t *__restrict__ rng) {
     const size_t nb = (size_t)blockIdx.x * N;
-    uint32_t u = 0, a = 0xFFFFFFFFu;
+    uint32_t u = 0, a = 0xFFFFFFFFu, oc = 0, om = 0;
     // NS_U nodes per thread in flight (one block per scenario: a single load triple per thread at
     // a time left the pass latency-bound, 0.23 ms for config 4's 4096 x 5k nodes)
     constexpr uint32_t NS_U = 4;
     for (uint32_t n0 = threadIdx.x; n0 < N; n0 += NS_U * blockDim.x) {
-        uint32_t l[NS_U], c[NS_U];
+        uint32_t l[NS_U], c[NS_U], x[NS_U], y[NS_U];
         uint8_t sc[NS_U];
 #pragma unroll
         for (uint32_t k = 0; k < NS_U; ++k) {
             const uint32_t n = n0 + k * blockDim.x;
             sc[k] = n < N ? sched[nb + n] : 0;
-            l[k] = n < N ? lab[nb + n] : 0u;
-            c[k] = n < N ? cu[nb + n] : 0xFFFFFFFFu;
+            if (SUMM) {
+                l[k] = n < N ? lab[nb + n] : 0u;
+                c[k] = n < N ? cu[nb + n] : 0xFFFFFFFFu;
+            }
+            if (RANGE) {
+                x[k] = n < N ? cf[nb + n] : 0u;
+                y[k] = n < N ? mf[nb + n] : 0u;
+            }
         }
 #pragma unroll
         for (uint32_t k = 0; k < NS_U; ++k) {
             if (sc[k]) {
-                u |= l[k];
-                a &= c[k];
+                if (SUMM) {
+                    u |= l[k];
+                    a &= c[k];
+                }
+                if (RANGE) {
+                    oc |= x[k];
+                    om |= y[k];
+                }
             }
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
         u |= (uint32_t)__shfl_xor((int)u, o);
         a &= (uint32_t)__shfl_xor((int)a, o);
+        oc |= (uint32_t)__shfl_xor((int)oc, o);
+        om |= (uint32_t)__shfl_xor((int)om, o);
     }
-    __shared__ uint32_t red[2][4];
+    __shared__ uint32_t red[4][4];
     const uint32_t w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][w] = u; red[1][w] = a; }
+    if ((threadIdx.x & 63) == 0) { red[0][w] = u; red[1][w] = a; red[2][w] = oc; red[3][w] = om; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (uint32_t q = 1; q < blockDim.x / 64; ++q) { u |= red[0][q]; a &= red[1][q]; }
-        summ[(size_t)blockIdx.x * 4] = u;
-        summ[(size_t)blockIdx.x * 4 + 1] = a;
+        for (uint32_t q = 1; q < blockDim.x / 64; ++q) { u |= red[0][q]; a &= red[1][q]; oc |= red[2][q]; om |= red[3][q]; }
+        if (SUMM) {
+            summ[(size_t)blockIdx.x * 4] = u;
+            summ[(size_t)blockIdx.x * 4 + 1] = a;
+        }
+        if (RANGE) {
+            if (oc) atomicOr(&rng[0], oc);
+            if (om) atomicOr(&rng[1], om);
+        }
     }
 }
 
@@ -1342,74 +1427,131 @@ size_t lds_bytes(uint32_t W, uint32_t G, uint32_t R) {
 }
 
 // G is a template parameter (records are register arrays); one instantiation per G
-template <uint32_t G, uint32_t BLK = 1024, uint32_t WV = 0>
+template <uint32_t G, uint32_t BLK = 1024, uint32_t WV = 0, bool PK = false>
 static int launch_g(hipStream_t st, unsigned grid, unsigned block, size_t lds, const PipeArgs &a) {
     if (block > BLK) return FP_EINVAL;
-    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe<G, BLK, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    FP_HIP(hipFuncSetAttribute((const void *)k_ffd_pipe<G, BLK, WV, PK>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    k_ffd_pipe<G, BLK, WV><<<grid, block, lds, st>>>(a);
+    k_ffd_pipe<G, BLK, WV, PK><<<grid, block, lds, st>>>(a);
     return FP_OK;
 }
 
 typedef int (*launch_fn)(hipStream_t, unsigned, unsigned, size_t, const PipeArgs &);
-// the kernels themselves (occupancy queries)
-#ifndef FPP_BIG_TU  // (fp_pipe_big.hip compiles only the 4096-scenario kernel, below)
-static const void *const kKernel[MAX_G + 1] = {
-    nullptr, (const void *)k_ffd_pipe<1, 1024>, (const void *)k_ffd_pipe<2, 1024>, (const void *)k_ffd_pipe<3, 1024>,
-    (const void *)k_ffd_pipe<4, 1024>, (const void *)k_ffd_pipe<5, 1024>, (const void *)k_ffd_pipe<6, 1024>,
-    (const void *)k_ffd_pipe<7, 1024>, (const void *)k_ffd_pipe<8, 1024>, (const void *)k_ffd_pipe<9, 1024>,
-    (const void *)k_ffd_pipe<10, 1024>, (const void *)k_ffd_pipe<11, 1024>, (const void *)k_ffd_pipe<12, 1024>,
-    (const void *)k_ffd_pipe<13, 1024>, (const void *)k_ffd_pipe<14, 1024>, (const void *)k_ffd_pipe<15, 1024>,
-    (const void *)k_ffd_pipe<16, 1024>};
+#ifndef FPP_KERNEL_TU  // (fp_pipe_tu.hip compiles one kernel of fp_pipe_tus.h, below)
+// The kernels of fp_pipe_tus.h: with FPP_SPLIT each lives in its own translation unit (fp_pipe_tu.hip,
+// the Makefile's FFD_TUS: each under its own LLVM machine scheduler) and is reached through its
+// launcher; without (the one-TU diagnostics build) they are instantiated here.
+struct TuKernel {
+    uint32_t G, BLK, WV, PK;
+    launch_fn launch;
+    const void *(*kernel)();
+};
+static_assert(WIDE12_BIG_WAVES == 6, "fp_pipe_tus.h names the six-wave 4096-scenario kernel");
+#ifdef FPP_SPLIT
+}  // namespace fpp
+#define FPP_TU_DECL(name, G, BLK, WV, PK)                                                    \
+    int fpp_tu_launch_##name(hipStream_t, unsigned, unsigned, size_t, const void *);         \
+    const void *fpp_tu_kernel_##name();
+FPP_TUS(FPP_TU_DECL)
+#undef FPP_TU_DECL
+namespace fpp {
+#define FPP_TU_ENTRY(name, G, BLK, WV, PK)                                                                     \
+    {G, BLK, WV, PK,                                                                                           \
+     [](hipStream_t st, unsigned gr, unsigned bl, size_t l, const PipeArgs &a) {                                \
+         return ::fpp_tu_launch_##name(st, gr, bl, l, &a);                                                    \
+     },                                                                                                        \
+     ::fpp_tu_kernel_##name},
+#else
+#define FPP_TU_ENTRY(name, G, BLK, WV, PK) \
+    {G, BLK, WV, PK, launch_g<G, BLK, WV, (bool)PK>, [] { return (const void *)k_ffd_pipe<G, BLK, WV, (bool)PK>; }},
+#endif
+static const TuKernel kTu[] = {FPP_TUS(FPP_TU_ENTRY)};
+#undef FPP_TU_ENTRY
+// (G, BLK, WV) has a u32 kernel in kTu: the tables below leave it out
+constexpr bool in_tu(uint32_t G, uint32_t BLK, uint32_t WV) {
+#define FPP_TU_IS(name, g, blk, wv, pk) || ((g) == G && (blk) == BLK && (wv) == WV && !(pk))
+    return false FPP_TUS(FPP_TU_IS);
+#undef FPP_TU_IS
+}
+static const TuKernel *tu_find(uint32_t G, uint32_t BLK, uint32_t WV, bool PK) {
+    for (const TuKernel &k : kTu)
+        if (k.G == G && k.BLK == BLK && k.WV == WV && (k.PK != 0) == PK) return &k;
+    return nullptr;
+}
+template <uint32_t G, uint32_t BLK = 1024, uint32_t WV = 0>
+static constexpr launch_fn main_launch() {
+    if constexpr (in_tu(G, BLK, WV)) return nullptr;
+    else return launch_g<G, BLK, WV>;
+}
+template <uint32_t G, uint32_t BLK = 1024, uint32_t WV = 0>
+static inline const void *main_kernel() {
+    if constexpr (in_tu(G, BLK, WV)) return nullptr;
+    else return (const void *)k_ffd_pipe<G, BLK, WV>;
+}
+// the u32 kernels not in kTu, by G: 1024-thread (multi-stage) and one-wave (wide) segments
 static const launch_fn kLaunch[MAX_G + 1] = {
-    nullptr,         launch_g<1>,  launch_g<2>,  launch_g<3>,  launch_g<4>,  launch_g<5>,
-    launch_g<6>,     launch_g<7>,  launch_g<8>,  launch_g<9>,  launch_g<10>, launch_g<11>,
-    launch_g<12>,    launch_g<13>, launch_g<14>, launch_g<15>, launch_g<16>};
+    nullptr,           main_launch<1>(),  main_launch<2>(),  main_launch<3>(),  main_launch<4>(),
+    main_launch<5>(),  main_launch<6>(),  main_launch<7>(),  main_launch<8>(),  main_launch<9>(),
+    main_launch<10>(), main_launch<11>(), main_launch<12>(), main_launch<13>(), main_launch<14>(),
+    main_launch<15>(), main_launch<16>()};
+static const void *const kKernel[MAX_G + 1] = {
+    nullptr,           main_kernel<1>(),  main_kernel<2>(),  main_kernel<3>(),  main_kernel<4>(),
+    main_kernel<5>(),  main_kernel<6>(),  main_kernel<7>(),  main_kernel<8>(),  main_kernel<9>(),
+    main_kernel<10>(), main_kernel<11>(), main_kernel<12>(), main_kernel<13>(), main_kernel<14>(),
+    main_kernel<15>(), main_kernel<16>()};
 // one-wave segments (W = 1) of 13..40 groups: G rounded up to a multiple of 4 (the padding
 // groups hold unschedulable records, which no container fits)
 constexpr uint32_t MAX_G_WIDE = 40;
 static const launch_fn kLaunchWide[MAX_G_WIDE / 4 + 1] = {
-    nullptr, nullptr, nullptr, launch_g<12, 64>, launch_g<16, 64>, launch_g<20, 64>,
-    launch_g<24, 64>, launch_g<28, 64>, launch_g<32, 64>, launch_g<36, 64>, launch_g<40, 64>};
+    nullptr, nullptr, nullptr, main_launch<12, 64>(), main_launch<16, 64>(), main_launch<20, 64>(),
+    main_launch<24, 64>(), main_launch<28, 64>(), main_launch<32, 64>(), main_launch<36, 64>(), main_launch<40, 64>()};
 static const void *const kKernelWide[MAX_G_WIDE / 4 + 1] = {
-    nullptr, nullptr, nullptr, (const void *)k_ffd_pipe<12, 64>,
-    (const void *)k_ffd_pipe<16, 64>, (const void *)k_ffd_pipe<20, 64>,
-    (const void *)k_ffd_pipe<24, 64>, (const void *)k_ffd_pipe<28, 64>, (const void *)k_ffd_pipe<32, 64>,
-    (const void *)k_ffd_pipe<36, 64>, (const void *)k_ffd_pipe<40, 64>};
+    nullptr, nullptr, nullptr, main_kernel<12, 64>(), main_kernel<16, 64>(), main_kernel<20, 64>(),
+    main_kernel<24, 64>(), main_kernel<28, 64>(), main_kernel<32, 64>(), main_kernel<36, 64>(), main_kernel<40, 64>()};
 static inline bool wide_g(uint32_t W, uint32_t G) { return W == 1 && G >= 12; }
 // the six-wave 12-group instantiation (WIDE12_BIG_S)
-#ifdef FPP_SPLIT_BIG
-// the 4096-scenario kernel (one-wave 12-group segments at six waves per SIMD) is compiled in its own
-// translation unit, fp_pipe_big.hip, under LLVM's iterative max-occupancy machine scheduler:
-// config-4 FFD 13.56 (iterative-ILP; 13.69 default) -> 13.21 ms with the same plans; on the rest of
-// this file no strategy beat the default beyond noise (profiles/r06o_sched_ab.txt)
-}  // namespace fpp
-int fpp_launch_wide12_big(hipStream_t st, unsigned grid, unsigned block, size_t lds, const void *args);
-const void *fpp_kernel_wide12_big();
-namespace fpp {
-static int launch_wide12_big(hipStream_t st, unsigned grid, unsigned block, size_t lds, const PipeArgs &a) {
-    return ::fpp_launch_wide12_big(st, grid, block, lds, &a);
-}
-static const launch_fn kLaunchWide12Big = launch_wide12_big;
-#define kKernelWide12Big (::fpp_kernel_wide12_big())
-#else
-static const launch_fn kLaunchWide12Big = launch_g<12, 64, WIDE12_BIG_WAVES>;
-static const void *const kKernelWide12Big = (const void *)k_ffd_pipe<12, 64, WIDE12_BIG_WAVES>;
-#endif
 static inline bool wide12_big(uint32_t S, uint32_t W, uint32_t G) { return W == 1 && G == 12 && S >= WIDE12_BIG_S; }
-#endif  // FPP_BIG_TU
+// The kernel of a geometry (PK: the packed one, if compiled; else null).  big: the six-wave
+// 12-group kernel (fp_pipe_launch takes it only with unbounded links).
+static void pipe_kernel(uint32_t G, uint32_t W, bool big, bool PK, launch_fn *l, const void **k) {
+    const bool wide = wide_g(W, G);
+    const uint32_t BLK = wide ? 64u : 1024u, WV = big ? WIDE12_BIG_WAVES : 0u;
+    *l = nullptr;
+    *k = nullptr;
+    if (const TuKernel *t = tu_find(G, BLK, WV, PK)) {
+        *l = t->launch;
+        *k = t->kernel();
+        return;
+    }
+    if (PK || big) return;
+    if (wide) {
+        if (G % 4 == 0 && G / 4 < sizeof(kLaunchWide) / sizeof(kLaunchWide[0])) {
+            *l = kLaunchWide[G / 4];
+            *k = kKernelWide[G / 4];
+        }
+    } else if (G < sizeof(kLaunch) / sizeof(kLaunch[0])) {
+        *l = kLaunch[G];
+        *k = kKernel[G];
+    }
+}
+#endif  // !FPP_KERNEL_TU
 
 }  // namespace fpp
 
-#ifdef FPP_BIG_TU
-// the one kernel and its launcher (this translation unit's namespace is renamed, fp_pipe_big.hip)
-int fpp_launch_wide12_big(hipStream_t st, unsigned grid, unsigned block, size_t lds, const void *args) {
-    return fpp::launch_g<12, 64, fpp::WIDE12_BIG_WAVES>(st, grid, block, lds, *static_cast<const fpp::PipeArgs *>(args));
+#ifdef FPP_KERNEL_TU
+// this translation unit's one kernel and its launcher (fp_pipe_tu.hip renames the namespace)
+#define FPP_TU_CAT2(a, b) a##b
+#define FPP_TU_CAT(a, b) FPP_TU_CAT2(a, b)
+int FPP_TU_CAT(fpp_tu_launch_, FPP_TU_NAME)(hipStream_t st, unsigned grid, unsigned block, size_t lds, const void *args) {
+    return fpp::launch_g<FPP_TU_G, FPP_TU_BLK, FPP_TU_WV, (bool)FPP_TU_PK>(st, grid, block, lds,
+                                                                          *static_cast<const fpp::PipeArgs *>(args));
 }
-const void *fpp_kernel_wide12_big() { return (const void *)fpp::k_ffd_pipe<12, 64, fpp::WIDE12_BIG_WAVES>; }
+const void *FPP_TU_CAT(fpp_tu_kernel_, FPP_TU_NAME)() {
+    return (const void *)fpp::k_ffd_pipe<FPP_TU_G, FPP_TU_BLK, FPP_TU_WV, (bool)FPP_TU_PK>;
+}
 #endif
 
-#ifndef FPP_BIG_TU
+#ifndef FPP_KERNEL_TU
 
 using namespace fpp;
 
@@ -1525,16 +1667,24 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     g->lds = lds_bytes(W, G, R);
     // resident segments on this device (0 if unknown)
     // (the kernel fp_pipe_launch will run: the six-wave one only with unbounded links)
+    // (and of its packed twin when there is one: the smaller of the two, either may run the batch)
     auto resident_of = [&](bool big) -> uint64_t {
-        int dev_cu = 0, occ = 0;
+        int dev_cu = 0;
         (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, c->device);
-        const bool wide = wide_g(W, G);
-        const void *fn = big ? kKernelWide12Big
-                         : wide ? (G / 4 < sizeof(kKernelWide) / sizeof(kKernelWide[0]) ? kKernelWide[G / 4] : nullptr)
-                                : (G < sizeof(kKernel) / sizeof(kKernel[0]) ? kKernel[G] : nullptr);
-        if (fn && dev_cu > 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), g->lds) == hipSuccess && occ > 0)
-            return (uint64_t)occ * (uint64_t)dev_cu;
-        return 0;
+        uint64_t res = 0;
+        for (const bool pk : {false, true}) {
+            launch_fn l;
+            const void *fn;
+            pipe_kernel(G, W, big, pk, &l, &fn);
+            int occ = 0;
+            if (!fn) continue;
+            if (dev_cu <= 0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (int)(W * 64), g->lds) != hipSuccess ||
+                occ <= 0)
+                return 0;
+            const uint64_t r = (uint64_t)occ * (uint64_t)dev_cu;
+            res = res && res < r ? res : r;
+        }
+        return res;
     };
     uint64_t slots_total = resident_of(wide12_big(S, W, G));
     g->resident = (uint32_t)(slots_total < 0xFFFFFFFFull ? slots_total : 0xFFFFFFFFull);
@@ -1623,7 +1773,7 @@ int fp_pipe_soa_take(fp_ctx *c, size_t SC, fp_pipe_soa *soa) {
 int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_base, const uint32_t *order,
                    const void *skeys, uint32_t key_bytes, uint32_t mbits, uint64_t cmax, uint64_t mmax,
                    const uint32_t *cval, const uint32_t *mval, const fp_batch *b, const uint32_t *thr,
-                   const fp_pipe_soa *ready) {
+                   const fp_pipe_soa *ready, uint32_t *rng) {
     PipeGeom geo;
     if (!pipe_geom(c, S, C, N, &geo)) return FP_EOVERFLOW;
     const uint32_t G = geo.G, W = geo.W, B = geo.B, R = geo.R, slots = geo.slots;
@@ -1652,7 +1802,20 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     if (N && fp_opt(c, FP_OPT_SCREEN, 1)) {
         summ = (uint32_t *)fp_ws_take(c, (size_t)S * 16);
         if (!summ) return FP_ENOMEM;
-        k_node_summary<<<S, 256, 0, st>>>(N, b->labels, b->conflict_used, b->schedulable, summ);
+    }
+    // the packed pair (fp_pipe_pk.h): the batch's node values join the containers' OR (rng, from the sort)
+    launch_fn u32fn = nullptr, pkfn = nullptr;
+    const bool big = wide12_big(S, W, G) && !geo.bounded;  // (idle flushes of global links need bounded)
+    {
+        const void *k_;
+        pipe_kernel(G, W, big, false, &u32fn, &k_);
+        if (rng && fp_opt(c, FP_OPT_PACKED, 1) != 0) pipe_kernel(G, W, big, true, &pkfn, &k_);
+        if (!u32fn) return FP_EOVERFLOW;
+    }
+    if (N && (summ || pkfn)) {
+        if (summ && pkfn) k_node_summary<true, true><<<S, 256, 0, st>>>(N, b->cpu_free, b->mem_free, b->labels, b->conflict_used, b->schedulable, summ, rng);
+        else if (summ) k_node_summary<true, false><<<S, 256, 0, st>>>(N, b->cpu_free, b->mem_free, b->labels, b->conflict_used, b->schedulable, summ, rng);
+        else k_node_summary<false, true><<<S, 256, 0, st>>>(N, b->cpu_free, b->mem_free, b->labels, b->conflict_used, b->schedulable, summ, rng);
         FP_HIP(hipGetLastError());
     }
     const int64_t pl_mode = fp_opt(c, FP_OPT_PAYLOAD_LDS, 1);
@@ -1738,9 +1901,23 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     }
     hipEvent_t ev;
     fp_prof_begin(c, FP_K_PLACE, &ev);
-    // the six-wave kernel is compiled for unbounded links only (see the kernel)
-    const bool big = wide12_big(S, W, G) && !geo.bounded && !(a.flush & 2u);
-    int rc = (big ? kLaunchWide12Big : wide ? kLaunchWide[G / 4] : kLaunch[G])(st, (unsigned)(S * B), W * 64, lds, a);
+    // the six-wave kernel is compiled for unbounded links only (see the kernel; `big` above)
+    int rc;
+    a.rng = rng;
+    if (pkfn) {
+        // the pair, back to back: the u32 kernel returns at once when the batch packs, the packed
+        // one when it does not (each reads the batch's OR words first)
+        a.pk_mode = 1;
+        rc = u32fn(st, (unsigned)(S * B), W * 64, lds, a);
+        if (!rc) {
+            FP_HIP(hipGetLastError());
+            a.pk_mode = 2;
+            rc = pkfn(st, (unsigned)(S * B), W * 64, lds, a);
+        }
+    } else {
+        a.pk_mode = 0;
+        rc = u32fn(st, (unsigned)(S * B), W * 64, lds, a);
+    }
     if (rc) return rc;
     FP_HIP(hipGetLastError());
     fp_prof_end(c, FP_K_PLACE, ev);
@@ -1829,4 +2006,4 @@ extern "C" int fp_debug_pipe_stats(unsigned long long *out, int reset) {
     return FP_OK;
 }
 #endif
-#endif  // !FPP_BIG_TU
+#endif  // !FPP_KERNEL_TU

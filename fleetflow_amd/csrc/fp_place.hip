@@ -45,7 +45,10 @@ constexpr uint32_t RANK_WORDS = RANK_MAX_VALUE / 32;
 // there) and ORed into the global bitmaps, nonzero words only.  A value >= 2^18 sets
 // cnt[CN_OVER] (the thresholds are then geometric).  The raw bounds come out of the same pass: cnt[CN_MAXC..CN_MINM]
 // (max cpu, max mem, smallest positive cpu, mem; the minima start at 0xFFFFFFFF).
-enum { CN_DC = 0, CN_DM = 1, CN_OVER = 6, CN_MAXC = 8, CN_MAXM = 9, CN_MINC = 10, CN_MINM = 11, CN_WORDS = 16 };
+// CN_ORC / CN_ORM: the OR of every cpu / mem value of the batch (containers here, schedulable nodes in
+// k_node_summary): the packed-capacity decision of k_ffd_pipe (fp_pipe_pk.h)
+enum { CN_DC = 0, CN_DM = 1, CN_OVER = 6, CN_MAXC = 8, CN_MAXM = 9, CN_MINC = 10, CN_MINM = 11, CN_ORC = 12, CN_ORM = 13,
+       CN_WORDS = 16 };
 __global__ __launch_bounds__(256) void k_value_bitmap(const uint32_t *__restrict__ cpu,
                                                       const uint32_t *__restrict__ mem, size_t n,
                                                       uint32_t *__restrict__ gbc, uint32_t *__restrict__ gbm,
@@ -162,13 +165,35 @@ __global__ __launch_bounds__(1024) void k_rank_tables(const uint32_t *__restrict
 
 // Radix-path keys: (~cpu << 32) | ~mem (descending demands sort ascending), value = the index in
 // the scenario.
-__global__ void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem, size_t n, uint32_t C,
-                            uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+// Also ORs every value into rng[0] (cpu) / rng[1] (mem): one atomic per block and word.
+__global__ __launch_bounds__(256) void k_make_keys(const uint32_t *__restrict__ cpu, const uint32_t *__restrict__ mem,
+                                                   size_t n, uint32_t C, uint64_t *__restrict__ keys,
+                                                   uint32_t *__restrict__ vals, uint32_t *__restrict__ rng) {
+    uint32_t oc = 0, om = 0;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = (uint32_t)i / C, j = (uint32_t)i - s * C;  // n = S * C < 2^32
-        keys[i] = ((uint64_t)~cpu[i] << 32) | (uint32_t)~mem[i];
+        const uint32_t c = cpu[i], m = mem[i];
+        keys[i] = ((uint64_t)~c << 32) | (uint32_t)~m;
         vals[i] = j;
+        oc |= c;
+        om |= m;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        oc |= (uint32_t)__shfl_xor((int)oc, o);
+        om |= (uint32_t)__shfl_xor((int)om, o);
+    }
+    __shared__ uint32_t red[2];
+    if (threadIdx.x < 2) red[threadIdx.x] = 0u;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        atomicOr(&red[0], oc);
+        atomicOr(&red[1], om);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (red[0]) atomicOr(&rng[0], red[0]);
+        if (red[1]) atomicOr(&rng[1], red[1]);
     }
 }
 
@@ -261,6 +286,7 @@ struct ScenSortArgs {
     const uint32_t *T;                       // [2 FP_BUCKETS] bucket thresholds (cpu, then mem; device)
     const uint32_t *scnt;                    // the sample's counts (CN_*)
     const unsigned char *simg;               // the sample's LDS image (k_sort_image), SS_IMG_BYTES
+    uint32_t *rng;                           // [2] the batch's OR of every cpu / mem value (CN_ORC)
 };
 
 // the u16 digit rows are also counted, zeroed and scanned through 32/64-bit views: these
@@ -456,6 +482,10 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     const size_t cb = (size_t)blockIdx.x * C;
     const uint32_t *cpu = a.cpu + cb, *mem = a.mem + cb;
     const unsigned long long ck0 = SS_CLK();
+    // the OR of every value this workgroup loads (pass 1's stream or A0: each sees the whole scenario)
+    __shared__ uint32_t ror[2];
+    uint32_t orc = 0, orm = 0;
+    if (t < 2) ror[t] = 0u;  // ordered before the atomics below by rank_pass's barriers
 
     // ---- R: the value set the digits rank against.  Pass 0 takes the sample's (k_value_bitmap
     // over the first THR_SAMPLE scenarios: a 64-KB copy from L2) when it has <= 256 values per
@@ -531,6 +561,8 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
                     const uint32_t i = t + blockDim.x * (k0 + k);
                     cv[k] = i < C ? __builtin_nontemporal_load(&cpu[i]) : 0u;
                     mv[k] = i < C ? __builtin_nontemporal_load(&mem[i]) : 0u;
+                    orc |= cv[k];
+                    orm |= mv[k];
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < SS_LB; ++k) {
@@ -612,6 +644,8 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
             for (uint32_t k = 0; k < SS_LB; ++k) {
                 const uint32_t p = s0 + 64 * (k0 + k) + lane;
                 const uint32_t c = cv[k], m = mv[k];
+                orc |= c;  // loads past the slice read the scenario's own values or 0: harmless
+                orm |= m;
                 // pass 0 copied the words up to the sample's largest values (all below 2^18)
                 if (p < s1 && (pass == 0 ? c > smc || m > smm : (c | m) >= RANK_MAX_VALUE)) miss = true;
                 else if (p < s1) {
@@ -637,6 +671,19 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     };
     uint32_t rr = samp ? rank_pass(0u) : 1u;
     if (rr == 1u) rr = rank_pass(1u);
+    for (int o = 32; o > 0; o >>= 1) {
+        orc |= (uint32_t)__shfl_xor((int)orc, o);
+        orm |= (uint32_t)__shfl_xor((int)orm, o);
+    }
+    if (lane == 0) {
+        atomicOr(&ror[0], orc);
+        atomicOr(&ror[1], orm);
+    }
+    __syncthreads();
+    if (t == 0) {
+        atomicOr(&a.rng[0], ror[0]);
+        atomicOr(&a.rng[1], ror[1]);
+    }
     if (rr == 2u) return;
     ss_offsets(WH, HS, HB, t, lane, w);
     const unsigned long long ck2 = SS_CLK();
@@ -874,6 +921,7 @@ int fp_place_ws_bytes_impl(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint64
 
 int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     const uint32_t S = b->n_scen, C = b->n_containers, N = b->n_nodes;
+    c->last_rng = nullptr;
     if (S == 0) return FP_OK;
     // the packed cost keeps 16 bits of the global scenario id (SPEC.md 2.4): more
     // scenarios would let a wrapped id win a tie it must lose
@@ -916,6 +964,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     if (!keys_in || !keys_out || !vals_in || !vals_out || !offs || !tmp || !rbm || !rpre || !rval || !rcnt || !thr ||
         !simg)
         return FP_ENOMEM;
+    c->last_rng = rcnt + CN_ORC;
 
     // ---- 1-2: the bucket thresholds (device), from the distinct values and bounds of a sample:
     // the first THR_SAMPLE scenarios (any ascending thresholds with T[0] = 0 are exact; they only
@@ -951,6 +1000,7 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         sa.order = vals_out; sa.s_cpu = soa.s_cpu; sa.s_mem = soa.s_mem; sa.s_idx = soa.s_idx;
         sa.T = thr;
         sa.scnt = rcnt;
+        sa.rng = rcnt + CN_ORC;
         sa.simg = simg;
         k_sort_image<<<1, 1024, 0, st>>>(rbm, rpre, rval, rcnt, thr, sa.kpack, simg);
         FP_HIP(hipGetLastError());
@@ -960,14 +1010,14 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
         FP_HIP(hipGetLastError());
         fp_prof_end(c, FP_K_SORT, ev);
         return fp_pipe_launch(c, S, C, N, b->scen_base, vals_out, nullptr, 4, 0, 0, 0, rval, rval + RANK_MAX_VALUE, b,
-                              thr, &soa);
+                              thr, &soa, rcnt + CN_ORC);
     }
     // ---- 3b: radix path: key = (~cpu << 32 | ~mem), value = the container's index; a stable
     // radix sort over all 64 bits gives (cpu desc, mem desc, index asc) without knowing the key
     // range on the host (FP_OPT_SEGSORT no longer changes anything: several scenarios are always
     // sorted as segments, one scenario device-wide) ----
     const uint64_t full = 0xFFFFFFFFull;
-    k_make_keys<<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, keys_in, vals_in);
+    k_make_keys<<<grid_for(SC, 256), 256, 0, st>>>(b->cpu_m, b->mem_mib, SC, C, keys_in, vals_in, rcnt + CN_ORC);
     FP_HIP(hipGetLastError());
     if (S == 1) {
         FP_HIP(rocprim::radix_sort_pairs(tmp, sort_tmp, keys_in, keys_out, vals_in, vals_out, SC, 0, 64, st));
@@ -980,7 +1030,17 @@ int fp_dev_place_batch_impl(fp_ctx *c, const fp_batch *b) {
     fp_prof_end(c, FP_K_SORT, ev);
     // ---- 4-5: placement + cost ----
     return fp_pipe_launch(c, S, C, N, b->scen_base, vals_out, keys_out, 8, 32, full, full, nullptr, nullptr, b, thr,
-                          nullptr);
+                          nullptr, rcnt + CN_ORC);
+}
+
+extern "C" int fp_ctx_place_path(fp_ctx *c, uint32_t *out3) {
+    if (!c || !out3) return FP_EINVAL;
+    out3[0] = out3[1] = out3[2] = 0u;
+    if (!c->last_rng) return FP_OK;
+    FP_HIP(hipSetDevice(c->device));
+    FP_HIP(hipStreamSynchronize(c->stream));
+    FP_HIP(hipMemcpy(out3, c->last_rng, 12, hipMemcpyDeviceToHost));
+    return FP_OK;
 }
 
 extern "C" int fp_dev_argmin_cost(fp_ctx *c, const uint64_t *cost, uint32_t n, uint32_t *best) {

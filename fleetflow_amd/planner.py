@@ -114,6 +114,13 @@ class Planner:
         check(self._L.fp_place_geometry(self._ctx, S, C, N, out), "fp_place_geometry")
         return dict(zip(_lib.GEOM_FIELDS, (int(x) for x in out)))
 
+    def place_path(self) -> dict:
+        """The FFD kernel the last placement ran (fp_ctx_place_path; waits for the stream):
+        {"or_cpu", "or_mem", "packed"} -- packed is True for the packed (cpu, mem) records."""
+        out = (ct.c_uint32 * 3)()
+        check(self._L.fp_ctx_place_path(self._ctx, out), "fp_ctx_place_path")
+        return {"or_cpu": int(out[0]), "or_mem": int(out[1]), "packed": int(out[2]) == 2, "ran": int(out[2]) != 0}
+
     def kernel_stats(self, kernel_id: int):
         ms = ct.c_double()
         n = ct.c_uint64()

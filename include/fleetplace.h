@@ -135,6 +135,10 @@ int fp_abi_version(void);
 enum { FP_K_PLACE = 0, FP_K_SORT = 1, FP_K_FEAS = 2, FP_K_LEVEL = 3, FP_K_GEN = 4, FP_K_COUNT = 5 };
 int fp_ctx_profile(fp_ctx *ctx, int enable);
 int fp_ctx_kernel_stats(fp_ctx *ctx, int kernel_id, double *total_ms, uint64_t *launches);
+/* The FFD kernel the last placement call on this context ran (waits for the stream): out[0] / out[1]
+ * = the OR of every cpu / mem value of its batch (containers and schedulable nodes), out[2] = 1 for
+ * the u32 records, 2 for the packed (cpu, mem) records (FP_OPT_PACKED), 0 if nothing ran. */
+int fp_ctx_place_path(fp_ctx *ctx, uint32_t *out3);
 
 /* Per-context tuning / test options.  FP_OPT_AUTO (-1) = the production choice (the
  * default of every option).  Nothing is read from the environment: an option changes
@@ -169,7 +173,9 @@ enum fp_option {
     FP_OPT_LEVEL_SMALL = 19,  /* 0 = no one-launch levelizer (<= 512 vertices) / legacy order (<= 1024) */
     FP_OPT_PIPE_PRIO = 20,    /* FFD wave priority: 0 off, 1 raised in the group loop, 2 for a batch's work */
     FP_OPT_INDEG_BIN = 21,    /* 0 = levelizer in-degrees by global atomics instead of binned in LDS */
-    FP_OPT_COUNT = 22
+    FP_OPT_PACKED = 22,       /* 0 = FFD on u32 records only; auto = packed (cpu, mem) records when the
+                                 batch's values fit them (decided on the device, fp_pipe_pk.h)  */
+    FP_OPT_COUNT = 23
 };
 int fp_ctx_set_option(fp_ctx *ctx, int option, int64_t value);
 int fp_ctx_get_option(fp_ctx *ctx, int option, int64_t *value);

@@ -44,6 +44,7 @@ pub const FP_OPT_LEVEL_SORT: c_int = 18;
 pub const FP_OPT_LEVEL_SMALL: c_int = 19;
 pub const FP_OPT_PIPE_PRIO: c_int = 20;
 pub const FP_OPT_INDEG_BIN: c_int = 21;
+pub const FP_OPT_PACKED: c_int = 22;
 pub const FP_GEOM_GROUPS: usize = 0;
 pub const FP_GEOM_STAGES: usize = 1;
 pub const FP_GEOM_SEGMENTS: usize = 2;
@@ -125,6 +126,7 @@ unsafe extern "C" {
     pub fn fp_abi_version() -> c_int;
     pub fn fp_ctx_profile(ctx: *mut fp_ctx, enable: c_int) -> c_int;
     pub fn fp_ctx_kernel_stats(ctx: *mut fp_ctx, kernel_id: c_int, total_ms: *mut f64, launches: *mut u64) -> c_int;
+    pub fn fp_ctx_place_path(ctx: *mut fp_ctx, out3: *mut u32) -> c_int;
     pub fn fp_ctx_set_option(ctx: *mut fp_ctx, option: c_int, value: i64) -> c_int;
     pub fn fp_ctx_get_option(ctx: *mut fp_ctx, option: c_int, value: *mut i64) -> c_int;
 

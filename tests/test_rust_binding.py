@@ -139,12 +139,32 @@ def test_build_script_runs_the_makefile_recipe():
     compiles = [c for c in base if " -c " in c]
     mk = open(os.path.join(ROOT, "fleetflow_amd", "csrc", "Makefile")).read()
     srcs = re.search(r"SRCS := (.*)", mk).group(1).split()
-    assert sorted(re.search(r" -c (\S+\.hip)", c).group(1) for c in compiles) == sorted(srcs + ["fp_pipe_big.hip"])
-    flags = {re.search(r" -c (\S+\.hip)", c).group(1): c for c in compiles}
-    assert "-DFPP_SPLIT_BIG" in flags["fp_pipe.hip"]
-    assert "--amdgpu-sched-strategy=" in flags["fp_pipe_big.hip"]
+    tus = _makefile_tus(mk)
+    objs = [c.split(" -o ")[1].split()[0] for c in compiles]
+    assert sorted(objs) == sorted([f"build/{s[:-4]}.o" for s in srcs] + [f"build/fp_pipe_tu_{t[0]}.o" for t in tus])
+    by_obj = dict(zip(objs, compiles))
+    assert "-DFPP_SPLIT" in by_obj["build/fp_pipe.o"]
+    for name, g, blk, wv, pk, sched in tus:
+        c = by_obj[f"build/fp_pipe_tu_{name}.o"]
+        assert f"-DFPP_TU_NAME={name} -DFPP_TU_G={g} -DFPP_TU_BLK={blk} -DFPP_TU_WV={wv} -DFPP_TU_PK={pk}" in c
+        assert (f"--amdgpu-sched-strategy={sched}" in c) == (sched != "default") and c.count("sched-strategy") <= 1
     link = [c for c in base if " -shared " in c and "../libfleetplace.so" in c]
-    assert len(link) == 1 and all(f"build/{s[:-4]}.o" in link[0] for s in srcs + ["fp_pipe_big.hip"])
+    assert len(link) == 1 and all(o in link[0] for o in objs)
+
+
+def _makefile_tus(mk):
+    body = re.search(r"FFD_TUS := ((?:.*\\\n)*.*)", mk).group(1).replace("\\\n", " ")
+    return [tuple(t.split(":")) for t in body.split()]
+
+
+def test_kernel_translation_units_match_the_header_list():
+    """The Makefile's FFD_TUS and fp_pipe_tus.h's FPP_TUS name the same kernels (name, G, BLK, WV,
+    PK): fp_pipe.hip (FPP_SPLIT) declares a launcher for every header entry, and only the Makefile
+    builds them."""
+    mk = open(os.path.join(ROOT, "fleetflow_amd", "csrc", "Makefile")).read()
+    hdr = open(os.path.join(ROOT, "fleetflow_amd", "csrc", "fp_pipe_tus.h")).read()
+    listed = re.findall(r"X\((\w+), (\d+), (\d+), (\d+), (\d+)\)", hdr)
+    assert listed and sorted(listed) == sorted(t[:5] for t in _makefile_tus(mk))
 
 
 def _calls(src, prefix="ffi::"):

@@ -82,6 +82,10 @@ for s in $steps; do
         --loads ${SWEEP_LOADS:-c4x512,c3} --reps 3 ${SWEEP_SET:+--set $SWEEP_SET} > ${log}_sweep_${SWEEP_OPT}.jsonl 2>&1 \
         || { echo "sweep failed"; tail -20 ${log}_sweep_${SWEEP_OPT}.jsonl; exit 1; }
       cut -c1-200 ${log}_sweep_${SWEEP_OPT}.jsonl | grep load ;;
+    ubench)
+      # one-wave group-loop microbenchmark (tools/ubench/systolic.hip, built on the CPU side)
+      timeout -k 10 120 tools/ubench/systolic > ${log}_ubench.txt 2>&1 || { echo "ubench failed"; tail ${log}_ubench.txt; exit 1; }
+      cat ${log}_ubench.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

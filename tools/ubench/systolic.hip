@@ -7,6 +7,8 @@
 //   pattern 2: config-3-like labels (4 one-hot dimensions), ports + anti-affinity
 //   pattern 3: a partly filled group (random free capacity), descending demands, 25% labels
 //   pattern 4: a full group: almost nothing fits (the pass-through case)
+// Variants 7-9 run the packed-capacity check (fp_pipe_pk.h) when the pattern's values pack
+// (every value a multiple of 2^sc and below 2^(15 + sc)); "n/a" otherwise.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../fleetflow_amd/csrc systolic.hip -o systolic
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -16,6 +18,7 @@
 #include "fp_pipe_sys.h"
 #include "fp_pipe_sysv.h"
 #include "fp_pipe_sysd.h"
+#include "fp_pipe_pk.h"
 
 using namespace fpp;
 
@@ -77,8 +80,32 @@ __global__ void k_sys(uint64_t *out, uint32_t *res, int pattern, uint32_t reps, 
         nxt = 0;
         const uint64_t q = ~0ull;
         __builtin_amdgcn_sched_barrier(0);
+        // packed form (V >= 7): shifts from the OR of every cpu / mem value of the pattern
+        uint32_t rw = 0, cw = 0, qw = 0, sc_c = 0, sc_m = 0;
+        bool pk_ok = true;
+        if constexpr (V >= 7) {
+            const uint32_t oc = sys_wave_or(rcf | cpu), om = sys_wave_or(rmf | mem);
+            sc_c = oc ? (uint32_t)__builtin_ctz(oc) : 0u;
+            sc_m = om ? (uint32_t)__builtin_ctz(om) : 0u;
+            pk_ok = (oc >> sc_c) <= PK_FIELD_MAX && (om >> sc_m) <= PK_FIELD_MAX;
+            rw = pk_pack(rcf, rmf, sc_c, sc_m);
+            cw = pk_pack(cpu, mem, sc_c, sc_m);
+            qw = pk_pack(qc, qm, sc_c, sc_m);
+            if (!pk_ok && lane == 0) out[63] = 1;  // not packable: reported n/a
+        }
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
-        if constexpr (V == 0) {
+        if constexpr (V >= 7) {
+            if (V == 7) {
+                fpp_group_xp<0, 1>(q, placed, touched, asg, nxt, rw, rcu, rlab, cw, req, conf, 1u, 0u, 0u, nchk, nhit, qw);
+            } else {
+                const uint32_t cap = V == 8 ? 1000u : (uint32_t)__builtin_popcountll(q) + extra;
+                SysOut so = fpp_sysp_group(q, touched, asg, rw, rcu, rlab, cw, req, conf, 0u, qw, cap);
+                uint64_t left = __builtin_amdgcn_readfirstlane((uint32_t)so.left) |
+                                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(so.left >> 32)) << 32);
+                if (left) fpp_asm_group_xp<false>(left, touched, asg, rw, rcu, rlab, cw, req, conf, 0u, nchk);
+                placed = __builtin_amdgcn_ballot_w64(asg != 0xFFFFFFFFu);
+            }
+        } else if constexpr (V == 0) {
             fpp_group_x<0, 1>(q, placed, touched, asg, nxt, rcf, rmf, rcu, rlab, cpu, mem, req, conf, 1u, 0u, 0u, nchk,
                               nhit, qc, qm);
         } else {
@@ -93,6 +120,10 @@ __global__ void k_sys(uint64_t *out, uint32_t *res, int pattern, uint32_t reps, 
         }
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (V >= 7) {  // records back to real units for the comparison with the serial loop
+            rcf = pk_cpu(rw, sc_c);
+            rmf = pk_mem(rw, sc_m);
+        }
         tot += t1 - t0;
         nplaced += __builtin_popcountll(placed);
         if (r == reps - 1 && threadIdx.x < 64) {
@@ -112,14 +143,15 @@ int main() {
     hipMalloc(&d, 64 * 8);
     hipMalloc(&dr, 5 * 64 * 4);
     const uint32_t reps = 64;
-    const char *names[7] = {"serial exec-masked (fpp_group_x)", "systolic, full", "systolic, Q+extra + serial",
-                           "VALU systolic, full", "VALU systolic, Q+extra + serial", "DPP-folded systolic, full",
-                           "DPP-folded, Q+extra + serial"};
+    const char *names[10] = {"serial exec-masked (fpp_group_x)", "systolic, full", "systolic, Q+extra + serial",
+                            "VALU systolic, full", "VALU systolic, Q+extra + serial", "DPP-folded systolic, full",
+                            "DPP-folded, Q+extra + serial", "packed serial (fpp_group_xp)", "packed systolic, full",
+                            "packed systolic, Q+extra + serial"};
     for (int pattern : {0, 1, 2, 3, 4}) {
         uint32_t ref[320], got[320];
-        for (int v = 0; v <= 6; ++v) {
+        for (int v = 0; v <= 9; ++v) {
             for (uint32_t extra : {0u, 8u, 16u}) {
-                if ((v < 2 || v == 3 || v == 5) && extra) continue;
+                if ((v < 2 || v == 3 || v == 5 || v == 7 || v == 8) && extra) continue;
                 for (int nw : {1, 4}) {
                     uint64_t h[64] = {0};
                     for (int it = 0; it < 2; ++it) {
@@ -130,13 +162,21 @@ int main() {
                         else if (v == 3) k_sys<3><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         else if (v == 4) k_sys<4><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         else if (v == 5) k_sys<5><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
-                        else k_sys<6><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else if (v == 6) k_sys<6><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else if (v == 7) k_sys<7><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else if (v == 8) k_sys<8><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
+                        else k_sys<9><<<1, nw * 64>>>(d, dr, pattern, reps, extra);
                         if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
                         hipMemcpy(h, d, 64 * 8, hipMemcpyDeviceToHost);
                     }
                     hipMemcpy(v == 0 ? ref : got, dr, sizeof(ref), hipMemcpyDeviceToHost);
                     int bad = 0;
                     if (v) for (int i = 0; i < 320; ++i) bad += ref[i] != got[i];
+                    if (h[63]) {
+                        printf("pattern %d %-34s extra %2u waves %d: n/a (values do not pack)\n", pattern, names[v],
+                               extra, nw);
+                        continue;
+                    }
                     printf("pattern %d %-34s extra %2u waves %d: %7.1f cycles per container (%llu placed of %u) "
                            "mismatches %d\n", pattern, names[v], extra, nw, (double)h[0] / (64.0 * reps),
                            (unsigned long long)h[1], 64 * reps, bad);
