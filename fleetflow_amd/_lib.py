@@ -126,6 +126,16 @@ def load():
     return _LIB
 
 
+def raw_function(name):
+    """A second handle to an export with no argtypes (no per-argument conversion on the call): the
+    caller passes ctypes objects only.  For the per-plan fast path (Planner.plan_stage_lists)."""
+    load()
+    f = getattr(ct.CDLL(LIB_PATH), name)
+    f.restype = ct.c_int
+    f.argtypes = None
+    return f
+
+
 def _lib_strerror(code):
     return load().fp_strerror(code).decode()
 

@@ -74,6 +74,7 @@ extern "C" void fp_ctx_destroy(fp_ctx *c) {
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_in_ev) (void)hipEventDestroy(c->h_in_ev);
     if (c->h_map) (void)hipHostFree(c->h_map);
+    if (c->h_tiny) (void)hipHostFree(c->h_tiny);
     if (c->lvl_q) (void)hipFree(c->lvl_q);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;

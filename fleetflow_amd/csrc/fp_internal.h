@@ -55,6 +55,11 @@ struct fp_ctx {
     char *h_map = nullptr;
     void *d_map = nullptr;
     size_t h_map_cap = 0;
+    // fp_plan_stage's one-wave path for stages of <= 64 services (k_plan_tiny): its tagged result
+    // words in mapped pinned host memory, and the tag of the last call (1..255)
+    char *h_tiny = nullptr;
+    void *d_tiny = nullptr;
+    uint32_t tiny_tag = 0;
     // the asynchronous levelizer's work queues (fp_order.hip), kept between calls: a clean finish
     // leaves them empty, and the flag in their last 256 bytes tells the next call whether to refill
     void *lvl_q = nullptr;

@@ -149,6 +149,13 @@ def stage_graph(services: list[str], flow: Flow):
     Vertex ids: first occurrence of each name in stage order.  Deps outside the
     target set add no edge (they count as satisfied).  Duplicate deps give
     duplicate edges.  Returns (vertex_names, pos_to_vertex, row_ptr, col, has_deps)."""
+    names, pos_to_vertex, row_ptr, col, has_deps = stage_graph_lists(services, flow)
+    return (names, np.array(pos_to_vertex, np.uint32), np.array(row_ptr, np.uint32), np.array(col, np.uint32),
+            np.frombuffer(has_deps, np.uint8))
+
+
+def stage_graph_lists(services: list[str], flow: Flow):
+    """stage_graph as plain lists (pos_to_vertex, row_ptr, col) and a bytearray (has_deps)."""
     vid: dict[str, int] = {}
     names: list[str] = []
     pos_to_vertex = []
@@ -181,8 +188,7 @@ def stage_graph(services: list[str], flow: Flow):
     for d, v in edges:
         col[fill[d]] = v
         fill[d] += 1
-    return (names, np.array(pos_to_vertex, np.uint32), np.array(row_ptr, np.uint32), np.array(col, np.uint32),
-            np.frombuffer(has_deps, np.uint8))
+    return names, pos_to_vertex, row_ptr, col, has_deps
 
 
 def levelize_stage(services: list[str], flow: Flow, planner: Planner | None = None):
@@ -276,6 +282,13 @@ def plan_stage(flow: Flow, stage_name: str, planner: Planner | None = None,
     assignment, rejected, candidates = {}, {}, {}
     if not services:
         return Plan(stage_name, [], {}, [], assignment, rejected, candidates)
+    if not nodes:
+        # no servers (the fleet.kdl fixtures): the graph stays in lists, one prebuilt call
+        names, pos2v, row_ptr, col, has_deps = stage_graph_lists(services, flow)
+        if len(names) == len(services):
+            perm, levels, order_v, _ = p.plan_stage_lists(row_ptr, col, has_deps)
+            return Plan(stage_name, [services[i] for i in perm], dict(zip(services, levels)),
+                        [services[i] for i in order_v], assignment, rejected, candidates)
     names, pos2v, row_ptr, col, has_deps = stage_graph(services, flow)
     if len(names) == len(services):
         cont, ntab = _stage_tables(names, flow, nodes) if nodes else (None, None)

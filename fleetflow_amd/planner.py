@@ -155,6 +155,38 @@ class Planner:
                                   order.ctypes.data_as(_lib.u32p), ct.byref(ncyc)), "fp_levelize")
         return level, order, ncyc.value
 
+    def plan_stage_lists(self, row_ptr, col, has_deps):
+        """fp_plan_stage without servers for a graph given as Python sequences (a fleet.kdl stage;
+        BASELINE config 1 is timed per plan, where numpy conversions and ctypes argument conversion
+        cost more than the GPU work): the inputs go into ctypes buffers kept between calls, the call
+        is one prebuilt foreign call, and the results come back as lists.  Returns (perm, level,
+        order, n_cycle).  Same checks and errors as plan_stage."""
+        V, E = len(has_deps), len(col)
+        self._need(V == 0 or len(row_ptr) == V + 1, "row_ptr must hold V + 1 entries")
+        fs = getattr(self, "_fs", None)
+        if fs is None or V > fs["V"] or E > fs["E"]:
+            cv, ce = max(64, V), max(256, E)
+            rp, cl, hd = (ct.c_uint32 * (cv + 1))(), (ct.c_uint32 * ce)(), (ct.c_uint8 * cv)()
+            out, ncyc = (ct.c_uint32 * (3 * cv))(), ct.c_uint32()
+            g = FpGraph(0, 0, ct.addressof(rp), ct.addressof(cl), ct.addressof(hd))
+            a = ct.addressof(out)
+            args = (self._ctx, ct.byref(g), None, None, ct.c_void_p(a), ct.c_void_p(a + 4 * cv),
+                    ct.c_void_p(a + 8 * cv), ct.byref(ncyc), None, None, None, None)
+            fs = self._fs = {"V": cv, "E": ce, "rp": rp, "col": cl, "hd": hd, "out": out, "ncyc": ncyc, "g": g,
+                             "args": args, "fn": _lib.raw_function("fp_plan_stage")}
+        if V == 0:
+            return [], [], [], 0
+        fs["rp"][:V + 1] = row_ptr
+        if E:
+            fs["col"][:E] = col
+        fs["hd"][:V] = has_deps
+        g = fs["g"]
+        g.n_vertices = V
+        g.n_edges = E
+        check(fs["fn"](*fs["args"]), "fp_plan_stage")
+        out, cv = fs["out"], fs["V"]
+        return out[:V], out[cv:cv + V], out[2 * cv:2 * cv + V], fs["ncyc"].value
+
     def plan_stage(self, row_ptr, col, has_deps, cont=None, nodes=None):
         """fp_plan_stage: one stage's A1 legacy order, A2 levels and start order and, with ``nodes``
         (container v = vertex v), the stage-2 candidates on the pristine table and the FFD plan gated

@@ -170,7 +170,8 @@ enum fp_option {
     FP_OPT_SYSTOLIC_VALU = 16,/* systolic step loop: 0 exec-masked, 1 VALU-only, auto/2 DPP-folded */
     FP_OPT_LINK_PUBLISH = 17, /* full slots per head publish on unbounded global links (auto 32) */
     FP_OPT_LEVEL_SORT = 18,   /* levelizer start order: 0 = radix sort, auto = LSD counting sort   */
-    FP_OPT_LEVEL_SMALL = 19,  /* 0 = no one-launch levelizer (<= 512 vertices) / legacy order (<= 1024) */
+    FP_OPT_LEVEL_SMALL = 19,  /* 0 = no one-launch levelizer (<= 512 vertices) / legacy order (<= 1024);
+                                 2 = fp_plan_stage without its one-wave path (<= 64 services)   */
     FP_OPT_PIPE_PRIO = 20,    /* FFD wave priority: 0 off, 1 raised in the group loop, 2 for a batch's work */
     FP_OPT_INDEG_BIN = 21,    /* 0 = levelizer in-degrees by global atomics instead of binned in LDS */
     FP_OPT_PACKED = 22,       /* 0 = FFD on u32 records only; auto = packed (cpu, mem) records when the

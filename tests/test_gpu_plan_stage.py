@@ -2,9 +2,11 @@
 
 Every output is checked against the C oracle on the same inputs: the A1 legacy order
 (engine.rs:67-85), the A2 levels and start order, the stage-2 candidates on the pristine table
-and the FFD plan gated by the levels' CYCLE (SPEC.md 2).  The one-kernel path (k_plan_small,
-<= 512 services / 8192 edges / 4096 servers) and the general path (a stage past the limits, or
-FP_OPT_LEVEL_SMALL = 0) must agree bit for bit.
+and the FFD plan gated by the levels' CYCLE (SPEC.md 2).  The one-wave path (k_plan_tiny, <= 64
+services / 256 edges / 64 servers, inputs in the kernel arguments), the one-workgroup path
+(k_plan_small, <= 512 services / 8192 edges / 4096 servers; FP_OPT_LEVEL_SMALL = 2 keeps it for
+the tiny shapes too) and the general path (a stage past the limits, or FP_OPT_LEVEL_SMALL = 0) must
+agree bit for bit.
 """
 import numpy as np
 import pytest
@@ -57,7 +59,8 @@ def _check(planner, O, rp, col, hd, cont=None, nodes=None):
     return level
 
 
-@pytest.mark.parametrize("V,E_extra,N", [(1, 0, 0), (3, 2, 0), (3, 2, 1), (40, 60, 7), (300, 2000, 64),
+@pytest.mark.parametrize("V,E_extra,N", [(1, 0, 0), (2, 0, 0), (3, 2, 0), (3, 2, 1), (40, 60, 7), (63, 150, 64),
+                                         (64, 200, 64), (64, 200, 65), (65, 30, 3), (300, 2000, 64),
                                          (511, 4000, 65), (512, 7000, 4096), (513, 500, 100), (700, 100, 0)])
 def test_plan_stage_vs_oracle(V, E_extra, N, planner, O, opts):
     rp, col, hd = _stage(V, E_extra, seed=V + N)
@@ -71,8 +74,42 @@ def test_plan_stage_vs_oracle(V, E_extra, N, planner, O, opts):
     lv = _check(planner, O, rp, col, hd, cont, nodes)
     if V >= 8:
         assert (lv == NONE).sum() >= 4  # the cycle, its tail and the self loop are CYCLE
-    opts(level_small=0)  # the general path: the same outputs
-    _check(planner, O, rp, col, hd, cont, nodes)
+    for mode in (2, 0):  # k_plan_small without the one-wave path; the general path: the same outputs
+        opts(level_small=mode)
+        _check(planner, O, rp, col, hd, cont, nodes)
+
+
+@pytest.mark.parametrize("E", [255, 256, 257])
+def test_plan_stage_tiny_edge_limit(E, planner, O, opts):
+    """The one-wave path takes at most 256 edges (u8 columns): 255 / 256 in it, 257 past it; duplicate
+    edges and a self loop included; the tag-polled results of consecutive calls stay distinct."""
+    V = 64
+    rng = np.random.default_rng(E)
+    a = rng.integers(0, V - 1, E - 1)
+    b = np.minimum(a + 1 + rng.integers(0, 9, E - 1), V - 1)
+    edges = list(zip(a.tolist(), b.tolist())) + [(40, 40)]
+    rp, col = _csr(V, edges)
+    hd = (rng.random(V) < 0.7).astype(np.uint8)
+    for _ in range(300):  # > 255 calls: the 8-bit tag wraps
+        _check(planner, O, rp, col, hd)
+    opts(level_small=2)
+    _check(planner, O, rp, col, hd)
+
+
+def test_plan_stage_tiny_corrupt_inputs(planner):
+    """Corrupt CSRs on the one-wave path: a column >= V (also one that a u8 cannot hold), a row_ptr
+    that does not end at E, a decreasing row and a row_ptr value past 16 bits -- FP_ECORRUPT, nothing
+    written, and the next call is fine."""
+    from fleetflow_amd import _lib
+    from fleetflow_amd._lib import FleetplaceError
+    cases = [([0, 1, 2], [0, 2]), ([0, 1, 2], [0, 300]), ([0, 1, 1], [1, 0]), ([0, 2, 1], [1, 0]),
+             ([0, 70000, 2], [1, 0])]
+    for rp, col in cases:
+        with pytest.raises(FleetplaceError) as ei:
+            planner.plan_stage(np.array(rp, np.uint32), np.array(col, np.uint32), np.array([1, 1], np.uint8))
+        assert ei.value.code == _lib.FP_ECORRUPT, (rp, col)
+    p, lv, od, nc, _ = planner.plan_stage([0, 1, 1], [1], [0, 1])
+    assert p.tolist() == [0, 1] and lv.tolist() == [0, 1] and od.tolist() == [0, 1] and nc == 0
 
 
 def test_plan_stage_limits_edges(planner, O):
