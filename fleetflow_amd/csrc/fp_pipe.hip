@@ -295,6 +295,12 @@ constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
 #endif
 // the systolic group fill (fp_pipe_sys.h) is compiled for stages of at most this many groups
 constexpr uint32_t SYS_MAX_G = 4;
+// ... and the packed one (fp_pipe_pk.h) for stages of at most this many (its records take one VGPR
+// fewer per group)
+#ifndef FPP_PK_SYS_MAX_G
+#define FPP_PK_SYS_MAX_G 4
+#endif
+constexpr uint32_t PK_SYS_MAX_G = FPP_PK_SYS_MAX_G;
 // The serial loop over one group's queue is the exec-masked loop (fp_pipe_asm.h fpp_group_x:
 // 172 vs 264 cycles per container for round 2's readlane / writelane loop).
 template <uint32_t G, bool UPD, bool IB, bool PK, uint32_t... gs, class Rec>
@@ -346,7 +352,7 @@ __device__ __forceinline__ void fpp_groups(std::integer_sequence<uint32_t, gs...
                 // long queues (a filling group): the systolic loop, else the serial one
                 // (compiled for the narrow stages only: the wide kernels stay within their VGPR budget)
                 if constexpr (PK) {
-                    if (G <= SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
+                    if (G <= PK_SYS_MAX_G && sys && (uint32_t)__builtin_popcountll(q) >= (sys & 0xFFFFu))
                         fpp_group_sysp<gs, G>(q, placed, touched, asg, nxt, rcf[gs], rcu[gs], rlab[gs], cw, req, conf,
                                               cand, cand_hi, gb64, nchk, nhit, qw, sys >> 16);
                     else
@@ -1731,7 +1737,7 @@ static bool pipe_geom(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, PipeGeom *g
     // Default: queues of >= 32 containers in the narrow stages (configs 2 / 3 / 5: one scenario,
     // one-group stages); config 3's k_ffd_pipe 72.1 -> 65.2 ms, config 2 0.81 -> 0.75 ms, every
     // threshold from 1 to 48 within 1 % (tools/sys_sweep.py, profiles/r03c_sys_sweep.jsonl)
-    g->sys = G <= SYS_MAX_G ? (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 32) : 0u;
+    g->sys = G <= (SYS_MAX_G > PK_SYS_MAX_G ? SYS_MAX_G : PK_SYS_MAX_G) ? (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC, 32) : 0u;
     if (g->sys > 64) g->sys = 64;
     g->sys_extra = (uint32_t)fp_opt(c, FP_OPT_SYSTOLIC_EXTRA, 16);
     if (g->sys_extra > 128) g->sys_extra = 128;
