@@ -326,7 +326,15 @@ def pmc_record(leg, S, C, N):
     return b, rec
 
 
-def roofline(leg, S, C, N, kernel_s, step_s):
+def _records(path):
+    """The FFD records the timed launches ran (fp_ctx_place_path, read after the timed region)."""
+    if not path or not path.get("ran"):
+        return None
+    return ("packed (cpu, mem) words, fp_pipe_pk.h" if path["packed"] else "u32 fields") + \
+        f" (batch OR cpu 0x{path['or_cpu']:x}, mem 0x{path['or_mem']:x})"
+
+
+def roofline(leg, S, C, N, kernel_s, step_s, path=None):
     """`achieved` / `frac` are ALGORITHMIC: the essential bytes of one launch (every container's
     16 B of demands read once + assign/reason written once, every node's 17 B read once + 12 B
     written back) over the kernel's live-timed duration.  The PMC counter bytes are `traffic`,
@@ -347,7 +355,8 @@ def roofline(leg, S, C, N, kernel_s, step_s):
            "traffic_frac": traffic / kernel_s / 1e9 / HBM_PEAK_GBPS if traffic else None,
            "traffic_source": (f"rocprofv3 PMC {rec.get('tag')}: 2 x FETCH_SIZE + WRITE_SIZE per launch, "
                               f"separate passes (profiles/pmc_latest.json)") if rec else None,
-           "kernel": "k_ffd_pipe (fleetflow_amd/csrc/fp_pipe.hip)", "kernel_ms": kernel_s * 1e3,
+           "kernel": "k_ffd_pipe (fleetflow_amd/csrc/fp_pipe.hip)", "records": _records(path),
+           "kernel_ms": kernel_s * 1e3,
            "work_equivalent": {"note": "16 B x S*C*N brute-force evaluations / kernel time: a work count, "
                                        "NOT bandwidth (pruned evaluations never touch memory)",
                                "evals_per_launch": S * C * N,
@@ -409,6 +418,7 @@ def single_leg(planner, dev, leg, seed, C, N, flags, steps, warmup, level_t=None
     k_ms, k_n = planner.kernel_stats(FP_K_PLACE)
     s_ms, s_n = planner.kernel_stats(FP_K_SORT)
     planner.profile(False)
+    path = planner.place_path()
     step_s = el / steps
     kernel_s = k_ms / max(k_n, 1) / 1e3
     reason = db.reason.cpu().numpy()
@@ -419,7 +429,7 @@ def single_leg(planner, dev, leg, seed, C, N, flags, steps, warmup, level_t=None
            "breakdown_ms": {"ffd_kernel": kernel_s * 1e3, "sort": s_ms / max(s_n, 1)},
            "ns_per_container": step_s / C * 1e9,
            "geometry": planner.geometry(1, C, N),
-           "roofline": roofline(leg, 1, C, N, kernel_s, step_s)}
+           "roofline": roofline(leg, 1, C, N, kernel_s, step_s, path)}
     del db, pristine
     torch.cuda.empty_cache()
     return out, plan
@@ -592,6 +602,7 @@ def worker(args):
     place_ms, place_n = planner.kernel_stats(FP_K_PLACE)
     sort_ms, sort_n = planner.kernel_stats(FP_K_SORT)
     planner.profile(False)
+    path = planner.place_path()
     # per-rank kernel time, max over ranks (the slowest rank sets the step)
     kt = torch.tensor([place_ms / max(place_n, 1), sort_ms / max(sort_n, 1)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -620,7 +631,7 @@ def worker(args):
                                    "winner plan broadcast from its owner",
                        "scenarios_total": S_total, "scenarios_per_gpu": S, "containers": C, "nodes": N,
                        "parallelism": f"scenario-sharded x{world}"},
-            "roofline": roofline("config4", S, C, N, kernel_ms / 1e3, step_s),
+            "roofline": roofline("config4", S, C, N, kernel_ms / 1e3, step_s, path),
             "breakdown_ms": {"ffd_kernel": kernel_ms, "sort": sort_avg_ms},
             "best_scenario": winner["best"], "best_owner_rank": winner["owner"],
         }

@@ -28,6 +28,19 @@ LEGS = [("config4", 4096, 50_000, 5_000), ("config2", 1, 10_000, 1_000), ("confi
 N_CONFIG3 = 2
 
 
+def dominant(rs, dur=None):
+    """The rows of the kernel instantiation that did the work: every leg launches the u32 / packed
+    k_ffd_pipe pair (fp_pipe_pk.h) with one grid, and the one whose values do not match returns at
+    once.  Kept: the name with the largest total duration (trace rows) or the largest counter total."""
+    tot = {}
+    for r in rs:
+        tot[r["Kernel_Name"]] = tot.get(r["Kernel_Name"], 0.0) + (dur(r) if dur else float(r["Counter_Value"]))
+    if not tot:
+        return rs
+    best = max(tot, key=tot.get)
+    return [r for r in rs if r["Kernel_Name"] == best]
+
+
 def rows(pattern):
     out = []
     for p in glob.glob(pattern, recursive=True):
@@ -74,11 +87,15 @@ def main():
         tr = trace.get(leg)
         if not tr:
             continue
+        tr = dominant(tr, lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        kname = tr[0]["Kernel_Name"]
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
-        f = statistics.mean(float(r["Counter_Value"]) for r in fetch[leg]) if fetch.get(leg) else None
-        w = statistics.mean(float(r["Counter_Value"]) for r in write[leg]) if write.get(leg) else None
+        fl = [r for r in fetch.get(leg, []) if r["Kernel_Name"] == kname]
+        wl = [r for r in write.get(leg, []) if r["Kernel_Name"] == kname]
+        f = statistics.mean(float(r["Counter_Value"]) for r in fl) if fl else None
+        w = statistics.mean(float(r["Counter_Value"]) for r in wl) if wl else None
         out[leg] = {
-            "kernel": KERNEL, "tag": tag, "S": S, "C": C, "N": N,
+            "kernel": KERNEL, "instantiation": kname, "tag": tag, "S": S, "C": C, "N": N,
             "grid_threads": int(tr[0]["Grid_Size_X"]),
             "launches_traced": len(durs),
             "avg_duration_ms": statistics.mean(durs) / 1e6,
