@@ -420,12 +420,31 @@ __device__ void ss_generic(const ScenSortArgs &a, uint16_t *X, uint16_t *WH, uin
         }
         __syncthreads();
     }
+    uint32_t oc = 0, om = 0;  // the batch's OR words (k_scen_sort)
     for (uint32_t P = t; P < C; P += blockDim.x) {
         const uint32_t j = __hip_atomic_load(&ord[P], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t cv = cpu[j], mv = mem[j];
         a.s_cpu[cb + P] = cv;
         a.s_mem[cb + P] = mv;
         a.s_idx[cb + P] = P | (a.kpack ? (ss_bucket(a.T, cv) << 21) | (ss_bucket(a.T + FP_BUCKETS, mv) << 26) : 0u);
+        oc |= cv;
+        om |= mv;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        oc |= (uint32_t)__shfl_xor((int)oc, o);
+        om |= (uint32_t)__shfl_xor((int)om, o);
+    }
+    __syncthreads();  // HS is free: every wave is past the last pass
+    if (t < 2) HS[t] = 0u;
+    __syncthreads();
+    if (lane == 0) {
+        atomicOr(&HS[0], oc);
+        atomicOr(&HS[1], om);
+    }
+    __syncthreads();
+    if (t == 0) {
+        atomicOr(&a.rng[0], HS[0]);
+        atomicOr(&a.rng[1], HS[1]);
     }
 }
 
@@ -482,10 +501,6 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     const size_t cb = (size_t)blockIdx.x * C;
     const uint32_t *cpu = a.cpu + cb, *mem = a.mem + cb;
     const unsigned long long ck0 = SS_CLK();
-    // the OR of every value this workgroup loads (pass 1's stream or A0: each sees the whole scenario)
-    __shared__ uint32_t ror[2];
-    uint32_t orc = 0, orm = 0;
-    if (t < 2) ror[t] = 0u;  // ordered before the atomics below by rank_pass's barriers
 
     // ---- R: the value set the digits rank against.  Pass 0 takes the sample's (k_value_bitmap
     // over the first THR_SAMPLE scenarios: a 64-KB copy from L2) when it has <= 256 values per
@@ -561,8 +576,6 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
                     const uint32_t i = t + blockDim.x * (k0 + k);
                     cv[k] = i < C ? __builtin_nontemporal_load(&cpu[i]) : 0u;
                     mv[k] = i < C ? __builtin_nontemporal_load(&mem[i]) : 0u;
-                    orc |= cv[k];
-                    orm |= mv[k];
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < SS_LB; ++k) {
@@ -644,8 +657,6 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
             for (uint32_t k = 0; k < SS_LB; ++k) {
                 const uint32_t p = s0 + 64 * (k0 + k) + lane;
                 const uint32_t c = cv[k], m = mv[k];
-                orc |= c;  // loads past the slice read the scenario's own values or 0: harmless
-                orm |= m;
                 // pass 0 copied the words up to the sample's largest values (all below 2^18)
                 if (p < s1 && (pass == 0 ? c > smc || m > smm : (c | m) >= RANK_MAX_VALUE)) miss = true;
                 else if (p < s1) {
@@ -671,20 +682,7 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
     };
     uint32_t rr = samp ? rank_pass(0u) : 1u;
     if (rr == 1u) rr = rank_pass(1u);
-    for (int o = 32; o > 0; o >>= 1) {
-        orc |= (uint32_t)__shfl_xor((int)orc, o);
-        orm |= (uint32_t)__shfl_xor((int)orm, o);
-    }
-    if (lane == 0) {
-        atomicOr(&ror[0], orc);
-        atomicOr(&ror[1], orm);
-    }
-    __syncthreads();
-    if (t == 0) {
-        atomicOr(&a.rng[0], ror[0]);
-        atomicOr(&a.rng[1], ror[1]);
-    }
-    if (rr == 2u) return;
+    if (rr == 2u) return;  // (ss_generic ORed the scenario's values into a.rng)
     ss_offsets(WH, HS, HB, t, lane, w);
     const unsigned long long ck2 = SS_CLK();
 
@@ -799,6 +797,23 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
 #else
     (void)ck0; (void)ck1; (void)ck2; (void)ck3; (void)big;
 #endif
+    // the batch's OR words (packed FFD records, fp_pipe_pk.h) from the value tables the digits rank
+    // against: the scenario's own distinct values, or the sample's (a superset of them, and values
+    // of the batch too) -- 2 x <= 256 LDS words by one wave, instead of registers kept live through
+    // A0 (that spilled 162 VGPRs); at the end, where the fewest registers are live
+    if (w == 0) {
+        uint32_t oc = 0, om = 0;
+        for (uint32_t i = lane; i < dc; i += 64) oc |= CV[i];
+        for (uint32_t i = lane; i < dm; i += 64) om |= MV[i];
+        for (int o = 32; o > 0; o >>= 1) {
+            oc |= (uint32_t)__shfl_xor((int)oc, o);
+            om |= (uint32_t)__shfl_xor((int)om, o);
+        }
+        if (lane == 0) {
+            atomicOr(&a.rng[0], oc);
+            atomicOr(&a.rng[1], om);
+        }
+    }
 }
 
 // T[0] = 0; T[1..31] spread evenly over the ascending distinct positive values v[0..d)
