@@ -78,10 +78,11 @@ for s in $steps; do
       done ;;
     sweep)
       # one context option over device-resident loads: SWEEP_OPT, SWEEP_VALUES, SWEEP_LOADS (tools/sys_sweep.py)
+      sw=${log}_sweep_${SWEEP_OPT}${SWEEP_SET:+_$(echo $SWEEP_SET | tr ',=' '__')}.jsonl
       timeout -k 10 400 python -u tools/sys_sweep.py --opt ${SWEEP_OPT:?} --values=${SWEEP_VALUES:?} \
-        --loads ${SWEEP_LOADS:-c4x512,c3} --reps 3 ${SWEEP_SET:+--set $SWEEP_SET} > ${log}_sweep_${SWEEP_OPT}.jsonl 2>&1 \
-        || { echo "sweep failed"; tail -20 ${log}_sweep_${SWEEP_OPT}.jsonl; exit 1; }
-      cut -c1-200 ${log}_sweep_${SWEEP_OPT}.jsonl | grep load ;;
+        --loads ${SWEEP_LOADS:-c4x512,c3} --reps 3 ${SWEEP_SET:+--set $SWEEP_SET} > $sw 2>&1 \
+        || { echo "sweep failed"; tail -20 $sw; exit 1; }
+      cut -c1-200 $sw | grep load ;;
     ubench)
       # one-wave group-loop microbenchmark (tools/ubench/systolic.hip, built on the CPU side)
       timeout -k 10 120 tools/ubench/systolic > ${log}_ubench.txt 2>&1 || { echo "ubench failed"; tail ${log}_ubench.txt; exit 1; }
