@@ -210,6 +210,12 @@ __device__ __forceinline__ uint32_t fpp_sysp_steps(uint32_t &xw, uint32_t &xu, u
 #if FPP_SP_UNROLL >= 16
             FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP
 #endif
+#if FPP_SP_UNROLL >= 24
+            FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP
+#endif
+#if FPP_SP_UNROLL >= 32
+            FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP FPP_SP_STEP
+#endif
             "s_nop 1"
             : [xw] "+v"(xw), [xu] "+v"(xu), [xl] "+v"(xl), [st] "+v"(st), [c] "+v"(c), [m] "+s"(m),
               [ta] "=&v"(ta), [tb] "=&v"(tb), [t] "=&v"(t), [d] "=&v"(d), [tu] "=&v"(tu)
