@@ -188,8 +188,11 @@ constexpr uint32_t PK_C0 = 0x40000000u;
     "v_cndmask_b32_e32 %[st], %[st], %[c], vcc\n\t"                  \
     "v_add_u32_e32 %[c], 1, %[c]\n\t"
 
+// steps per exit check (one ballot + branches): 16.  Config 3's kernel 50.4-50.8 (8) -> 47.2-47.8 ms
+// (16), 47.4-47.7 (24), 49.7-49.8 (32), 58.0 (4); config 2 0.70 -> 0.66 ms (profiles/r07f_*, r07g_*):
+// a check costs more than the steps a longer block wastes at the end of a queue
 #ifndef FPP_SP_UNROLL
-#define FPP_SP_UNROLL 8
+#define FPP_SP_UNROLL 16
 #endif
 
 // Runs steps (in blocks of FPP_SP_UNROLL) until every container has started and none is still

@@ -102,6 +102,9 @@ __device__ __forceinline__ uint32_t fpp_sysd_steps(uint32_t &xc, uint32_t &xm, u
 #if FPP_SD_UNROLL >= 8
             FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP
 #endif
+#if FPP_SD_UNROLL >= 16
+            FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP FPP_SD_STEP
+#endif
             "s_nop 1"
             : [xc] "+v"(xc), [xm] "+v"(xm), [xu] "+v"(xu), [xl] "+v"(xl), [k] "+v"(k), [apos] "+v"(apos),
               [dv] "=&v"(dv), [ta] "=&v"(ta), [tb] "=&v"(tb), [t] "=&v"(t), [d1] "=&v"(d1), [d2] "=&v"(d2),
