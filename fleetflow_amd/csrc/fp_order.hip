@@ -504,15 +504,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
     uint32_t pofs[kPush], pbase = 0, npend = 0;
     uint64_t pent[kPush];
     uint64_t *pq = Q;
-    // a join child's first edge record (and hops), loaded beside the CAS that may make the child
-    // ready: when this lane continues at that child from its first edge next round, the record is
-    // already here -- one round trip per join level on the chain instead of two (speculative: unused
-    // when another lane's CAS completes the join, or the lane continues elsewhere)
-    bool spq = false;
-    uint32_t spu_w = 0, spu_e = 0;
-    uint4 spv = make_uint4(0u, 0u, 0u, 0u), sph[kHops - 1];
-#pragma unroll
-    for (uint32_t h = 0; h + 1 < kHops; ++h) sph[h] = make_uint4(0u, 0u, 0u, 0u);
+    // (Round 6 tried loading a join child's first edge record beside the CAS that may make it ready,
+    // to save a round trip per join level on the chain: k_lvl_async 495 -> 540 us on config 5,
+    // profiles/r07h_lvl_prefetch_kernel_stats.csv -- the extra loads of every join edge cost more than they saved.)
     while (true) {
         // one round: the poll of a claimed slot and one edge step of an item are issued
         // together, so a busy wave's polls cost no extra round trip
@@ -583,14 +577,12 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         // were serial round trips per hop
         const uint32_t ne = has_item ? min(e1 - e, kLaneEdges) : 0u;
         uint4 erv[kLaneEdges], erh[kHops - 1];
-        const bool use_sp = spq && ne && u == spu_w && e == spu_e;  // last round's speculative load
-        spq = false;
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k)
-            if (k < ne) erv[k] = (k == 0 && use_sp) ? spv : erec[e + k];
+            if (k < ne) erv[k] = erec[e + k];
 #pragma unroll
         for (uint32_t h = 0; h + 1 < kHops; ++h)  // the hops after edge e (k_edge_rec), same round trip
-            erh[h] = use_sp ? sph[h] : (pk && ne) ? erec2[(size_t)h * E + e] : make_uint4(0u, 0u, 0u, 0u);
+            erh[h] = (pk && ne) ? erec2[(size_t)h * E + e] : make_uint4(0u, 0u, 0u, 0u);
         if (npend) {
             const uint32_t base = __shfl(pbase, 0);
 #pragma unroll
@@ -620,16 +612,6 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                            ? gn : kQEmpty;
                 }
-            }
-            // the speculative load (after the CAS, so that waiting for the CAS does not wait for it)
-            if (ne && !only[0] && p1[0] > p0[0] && p0[0] < E) {
-                spq = true;
-                spu_w = w[0];
-                spu_e = p0[0];
-                spv = erec[p0[0]];
-#pragma unroll
-                for (uint32_t h = 0; h + 1 < kHops; ++h)
-                    sph[h] = pk ? erec2[(size_t)h * E + p0[0]] : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
             for (uint32_t k = 0; k < kLaneEdges; ++k) {

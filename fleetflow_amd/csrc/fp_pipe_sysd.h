@@ -21,10 +21,11 @@
 
 namespace fpp {
 
-// steps per exit check (one ballot + two branches): 8 (pattern 0-3 of tools/ubench/systolic.hip: 109-138
-// cycles per container against 122-156 with 4, profiles/r05e_sysd_ubench.txt)
+// steps per exit check (one ballot + two branches): 16 (round 6: config 3 on the u32 kernels 55.9 ->
+// 54.4-54.8 ms, config 2 0.77 -> 0.75 ms against 8, profiles/r07h_u32_unroll16_ab.jsonl; round 5: 8
+// against 4, patterns 0-3 of tools/ubench/systolic.hip 109-138 vs 122-156 cycles per container)
 #ifndef FPP_SD_UNROLL
-#define FPP_SD_UNROLL 8
+#define FPP_SD_UNROLL 16
 #endif
 
 #define FPP_SD_DPP " wave_ror:1 row_mask:0xf bank_mask:0xf\n\t"
