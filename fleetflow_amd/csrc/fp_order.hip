@@ -212,9 +212,14 @@ __global__ void k_lvl_final(const uint32_t *__restrict__ indeg, uint32_t V, uint
 // Termination: done[] counts queue items whose lane (and continuation chain) has
 // finished, tail[] counts pushed items; done == tail means nothing is in flight and
 // nothing can be pushed again.  One monitor lane checks it and raises `fin`.
-constexpr uint32_t kShards = 8;           // queues (blocks b and b+8 share an XCD)
+#ifndef LVL_SHARDS
+#define LVL_SHARDS 8
+#endif
+// queues (blocks b and b+8 share an XCD); 16 queues: config 5 -1 %, 32: +2 % (profiles/r07n_lvl_ab.txt)
+constexpr uint32_t kShards = LVL_SHARDS;
 constexpr uint32_t kCtlStride = 32;       // u32 words between counters (128 B lines)
-constexpr uint32_t kMaxLevelWord = 26 * kCtlStride;  // ctl word: the largest level the schedule wrote
+constexpr uint32_t kFinWord = 3 * kShards * kCtlStride, kAbortWord = kFinWord + kCtlStride;
+constexpr uint32_t kMaxLevelWord = kAbortWord + kCtlStride;  // ctl word: the largest level the schedule wrote
 constexpr uint64_t kQEmpty = ~0ull;
 // edges left at which the wave expands a vertex together, and edges a lane relaxes per round
 // (config 5: 16 / 1 0.775 ms; cooperative at 8 0.823, at 32 0.779; 2 edges per lane 0.877;
@@ -222,17 +227,50 @@ constexpr uint64_t kQEmpty = ~0ull;
 constexpr uint32_t kCoopEdges = 16;
 constexpr uint32_t kLaneEdges = 1;
 // levels a lane may jump per round along only-parent first edges: 4 (config 5 0.84 ms; 6 hops 0.86, 8 hops
-// 0.92 -- more records to build and load per round, profiles/r04m_lvl_hops_ab.txt)
-constexpr uint32_t kHops = 4;
+// 0.92 -- more records to build and load per round, profiles/r04m_lvl_hops_ab.txt; round 6 at 16-B queue
+// entries: 4 / 6 / 8 hops 0.663-0.665 / 0.664-0.665 / 0.738 ms, profiles/r07p_lvl_ab.txt)
+#ifndef LVL_HOPS
+#define LVL_HOPS 4
+#endif
+constexpr uint32_t kHops = LVL_HOPS;
 constexpr uint32_t kPush = kLaneEdges + kHops;  // queue entries a lane may push per round
 // one-wave blocks of the persistent grid: 8 waves per CU (config 5: 2048 0.78 ms, 512 0.84, 4096 0.79,
 // 8192 0.81, 256 0.92; profiles/r04v_lvl_grid_ab.txt) -- a wave round lasts as long as its slowest
 // lane, so spreading the items over more waves shortens the rounds of the lanes on the long chains,
 // until idle waves' queue polls start to cost more
 constexpr uint32_t kAsyncBlocks = 2048;
-// ctl layout (u32 index): head[s] = s*32, tail[s] = (8+s)*32, done[s] = (16+s)*32,
-// fin = 24*32, abort = 25*32, maxlvl = 26*32
-constexpr uint32_t kCtlWords = 27 * kCtlStride;
+#ifndef LVL_SLEEP_LONG
+#define LVL_SLEEP_LONG 8  // s_sleep of an idle wave after LVL_IDLE_SPIN short (s_sleep 1) rounds (2 / 32: +-1 %, r07k)
+#endif
+#ifndef LVL_IDLE_SPIN
+#define LVL_IDLE_SPIN 16
+#endif
+// ctl layout (u32 index, S = kShards): head[s] = s*32, tail[s] = (S+s)*32, done[s] = (2S+s)*32,
+// fin = 3S*32, abort = (3S+1)*32, maxlvl = (3S+2)*32
+constexpr uint32_t kCtlWords = kMaxLevelWord + kCtlStride;
+
+// Diagnostics build only (-DFP_LVL_TRACE, tools/lvl_trace.py): the first time each level is
+// written by k_lvl_async (s_memrealtime, 100 MHz), [4094] the earliest wave start, [4095] the last
+// wave exit.  Read back with fp_debug_lvl_trace.
+#ifdef FP_LVL_TRACE
+__device__ unsigned long long g_lvl_trace[4096];
+// (a lane keeps the deepest level it wrote in a round with its time; the next round loads that
+// level's word beside its records and lowers it only when this lane was first, so the hot words
+// of the last levels see few atomics -- an atomic per write slowed config 5 from 0.5 to 2.3 ms)
+#define LVL_TR(L)                                                                                        \
+    do {                                                                                                 \
+        if ((L) > my_max && (trL == FP_NONE || (L) > trL)) {                                             \
+            trL = min((uint32_t)(L), 4093u);                                                             \
+            trT = __builtin_amdgcn_s_memrealtime();                                                      \
+        }                                                                                                \
+    } while (0)
+extern "C" __attribute__((visibility("default"))) int fp_debug_lvl_trace(uint64_t *out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lvl_trace), sizeof(g_lvl_trace)) == hipSuccess ? 0 : -1;
+}
+#else
+#define LVL_TR(L) ((void)0)
+#endif
 
 __device__ __forceinline__ uint64_t ag_ld64(const uint64_t *p) {
     return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -261,7 +299,7 @@ __device__ __forceinline__ uint32_t ag_rmw_rd(uint32_t *p) {  // coherent read (
 // depth D takes ~D / kHops rounds.  (Two levels per round: config-5 levelize 1.51 -> 1.13 ms.)
 
 // ---- the async path's set-up in four launches (round 5; was 12 launches and memsets) -----------
-// The work queues (kShards x V u64, 64 MB at config 5) live in a context buffer of their own
+// The work queues (kShards x V 16-B entries, 128 MB at config 5) live in a context buffer of their own
 // (fp_ctx::lvl_q): k_lvl_async resets every slot it consumes, so a levelization that finishes
 // cleanly leaves them empty and marks the buffer clean (qflag = kQClean); the next call fills them
 // with kQEmpty only when the flag says otherwise (a fresh buffer, an aborted or corrupt call).
@@ -411,7 +449,7 @@ __global__ __launch_bounds__(kHistT) void k_indeg_hist(const uint32_t *__restric
 __global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__restrict__ indeg,
                            const uint32_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t V,
                            uint32_t E, uint32_t vblocks, uint32_t *__restrict__ level, uint64_t *__restrict__ state,
-                           uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl, bool pk, uint4 *__restrict__ rec,
+                           uint4 *__restrict__ Q, uint32_t *__restrict__ ctl, uint4 *__restrict__ rec,
                            const uint4 *__restrict__ vrec, const uint32_t *__restrict__ bad) {
     if (*bad) return;
     if (blockIdx.x < vblocks) {
@@ -434,9 +472,9 @@ __global__ void k_lvl_prep(const uint8_t *__restrict__ hd, const uint32_t *__res
         uint32_t base = 0;
         if (lane == leader) base = atomicAdd(&ctl[(kShards + sh) * kCtlStride], (uint32_t)__popcll(m));
         base = __shfl(base, (int)leader);
-        if (push)
+        if (push)  // a 16-B queue entry (k_lvl_async): (level << 32 | v, first edge << 32 | end edge)
             Q[(size_t)sh * V + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
-                ((uint64_t)(pk ? l0 << 8 : l0) << 32) | v;
+                make_uint4((uint32_t)v, l0, row_ptr[v + 1], row_ptr[v]);
         return;
     }
     const size_t st = (size_t)(gridDim.x - vblocks) * blockDim.x;
@@ -478,43 +516,116 @@ __global__ void k_edge_hops(uint32_t E, const uint4 *__restrict__ rec, uint4 *__
     }
 }
 
-__global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ row_ptr, const uint4 *__restrict__ erec,
-                                                  const uint4 *__restrict__ erec2, uint32_t E, uint32_t V, uint64_t *__restrict__ state, uint64_t *__restrict__ Q,
-                                                  uint32_t *__restrict__ ctl, uint32_t *__restrict__ level,
-                                                  uint32_t *__restrict__ err, bool pk,
+// Queue entries are 16 B: lo = (level << 32) | vertex, hi = (first edge << 32) | end edge, so a lane
+// that claims an item has its edge range with it (no row_ptr round trip).  Only vertices with edges
+// left are pushed (a ready child without out-edges is final where it becomes ready), so a valid hi
+// has first edge < end edge <= E and is never the empty marker; an entry is taken only when both
+// halves are valid (the producer's two stores may land in either order).
+struct QEnt {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ QEnt q_ent(uint32_t v, uint32_t lvl, uint32_t e0, uint32_t e1) {
+    return QEnt{((uint64_t)lvl << 32) | v, ((uint64_t)e0 << 32) | e1};
+}
+__device__ __forceinline__ void q_store(uint64_t *slot2, const QEnt &x) {
+    __hip_atomic_store(slot2 + 1, x.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(slot2, x.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec, const uint4 *__restrict__ erec2,
+                                                  uint32_t E, uint32_t V, uint64_t *__restrict__ state,
+                                                  uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
+                                                  uint32_t *__restrict__ level, uint32_t *__restrict__ err,
                                                   const uint32_t *__restrict__ bad, uint32_t *__restrict__ qflag) {
     if (*bad) return;  // a corrupt CSR: no expansion (uniform: every block leaves)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sh = blockIdx.x % kShards;
     uint32_t *head = &ctl[sh * kCtlStride];
     uint32_t *done = &ctl[(2 * kShards + sh) * kCtlStride];
-    uint32_t *fin = &ctl[24 * kCtlStride], *abortw = &ctl[25 * kCtlStride];
-    const uint64_t *q = Q + (size_t)sh * V;  // claims come from the block's own shard
-    uint32_t rr = blockIdx.x / kShards;       // pushes rotate over all shards (load spreading)
+    uint32_t *fin = &ctl[kFinWord], *abortw = &ctl[kAbortWord];
+    uint64_t *q = Q + (size_t)sh * V * 2;  // claims come from the block's own shard (2 words a slot)
+    uint32_t rr = blockIdx.x / kShards;    // pushes rotate over all shards (load spreading)
     const bool monitor = blockIdx.x == 0;
     const uint64_t lt = (1ull << lane) - 1ull;
     // lane state: a claim on a queue slot, or an item u (level lu) with edges [e, e1),
-    // and at most one continuation cw (level cl, edges [ce, ce1) prefetched)
+    // and at most one continuation cw (level cl, edges [ce, ce1))
     bool has_claim = false, has_item = false;
     uint32_t slot = 0, u = 0, lu = 0, e = 0, e1 = 0, my_max = 0, idle = 0;
-    uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0, eb = 0;  // eb: first edge of u
+    uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     // deferred pushes (see below): entries, offsets, the reserved base (lane 0)
     bool pend[kPush];
     uint32_t pofs[kPush], pbase = 0, npend = 0;
-    uint64_t pent[kPush];
+    QEnt pent[kPush];
     uint64_t *pq = Q;
+    // deferred claims: the reservation's result (leader lane), the leader, this lane's rank
+    bool cpend = false;
+    uint32_t cbase = 0, cleader = 0, crank = 0;
+#ifdef FP_LVL_TRACE
+    uint32_t trL = FP_NONE;
+    uint64_t trT = 0;
+#endif
     // (Round 6 tried loading a join child's first edge record beside the CAS that may make it ready,
     // to save a round trip per join level on the chain: k_lvl_async 495 -> 540 us on config 5,
     // profiles/r07h_lvl_prefetch_kernel_stats.csv -- the extra loads of every join edge cost more than they saved.)
+    //
+    // A round issues everything it will wait for first -- the edge records, then the polls of
+    // claimed slots -- and only then waits: for the previous round's push and claim reservations,
+    // the cooperative expansions and the records.  A wave's memory operations complete in order, so
+    // any dependent load issued later in the round (round 5 loaded a claimed item's row_ptr pair,
+    // then the next round's records behind it) stalls every lane of the wave, the lanes walking
+    // chains included.
     while (true) {
-        // one round: the poll of a claimed slot and one edge step of an item are issued
-        // together, so a busy wave's polls cost no extra round trip
-        uint64_t x = kQEmpty;
-        if (has_claim && slot < V) x = ag_ld64(&q[slot]);
-        // a vertex with many edges left (a chain head feeding a whole fan-out layer) is
-        // expanded by the whole wave, 64 edges per step, its ready children all pushed
-        uint64_t bm = __ballot(has_item && e1 - e >= kCoopEdges);
+        // a vertex with many edges left (a chain head feeding a whole fan-out layer) is expanded by
+        // the whole wave, 64 edges per step (below); the others take one edge step per lane
+        const bool coop = has_item && e1 - e >= kCoopEdges;
+        uint64_t bm = __ballot(coop);
+        bool ready[kLaneEdges], fin_item = false, part = false;
+        bool jp[kHops - 1];  // a vertex passed by a jump has edges left: queue them
+        QEnt jent[kHops - 1];
+#pragma unroll
+        for (uint32_t h = 0; h + 1 < kHops; ++h) jp[h] = false;
+        QEnt pent_part{0, 0};
+        uint32_t w[kLaneEdges], wl[kLaneEdges], p0[kLaneEdges], p1[kLaneEdges];
+#pragma unroll
+        for (uint32_t k = 0; k < kLaneEdges; ++k) ready[k] = false;
+        const uint32_t ne = has_item && !coop ? min(e1 - e, kLaneEdges) : 0u;
+        uint4 erv[kLaneEdges], erh[kHops - 1];
+#pragma unroll
+        for (uint32_t k = 0; k < kLaneEdges; ++k)
+            if (k < ne) erv[k] = erec[e + k];
+#pragma unroll
+        for (uint32_t h = 0; h + 1 < kHops; ++h)  // the hops after edge e (k_edge_hops), same round trip
+            erh[h] = ne ? erec2[(size_t)h * E + e] : make_uint4(0u, 0u, 0u, 0u);
+#ifdef FP_LVL_TRACE
+        const uint32_t trL0 = trL;
+        const uint64_t trT0 = trT;
+        unsigned long long trV = 0;
+        if (trL0 != FP_NONE) trV = __hip_atomic_load(&g_lvl_trace[trL0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        trL = FP_NONE;
+#endif
+        // the poll of a claimed slot, behind the records
+        QEnt x{kQEmpty, kQEmpty};
+        if (has_claim && slot < V) {
+            x.lo = ag_ld64(&q[2 * (size_t)slot]);
+            x.hi = ag_ld64(&q[2 * (size_t)slot + 1]);
+        }
+        // the previous round's reservations: pushes stored, claims become slots (polled next round)
+        if (npend) {
+            const uint32_t base = __shfl(pbase, 0);
+#pragma unroll
+            for (uint32_t k = 0; k < kPush; ++k)
+                if (pend[k]) q_store(pq + 2 * (size_t)(base + pofs[k]), pent[k]);
+            npend = 0;
+        }
+        if (__ballot(cpend)) {
+            const uint32_t b = __shfl(cbase, (int)cleader);
+            if (cpend) {
+                slot = b + crank;
+                has_claim = true;
+                cpend = false;
+            }
+        }
         while (bm) {
             const uint32_t L = (uint32_t)__builtin_ctzll(bm);
             bm &= bm - 1;
@@ -523,11 +634,11 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             for (uint32_t base = be0; base < be1; base += 64) {
                 const uint32_t ee = base + lane;
                 bool rdy = false;
-                uint32_t ww = 0;
+                uint32_t ww = 0, r0 = 0, r1 = 0;
                 uint64_t cur = 0;
                 if (ee < be1) {
                     const uint4 er = erec[ee];
-                    ww = er.x;
+                    ww = er.x; r0 = er.y; r1 = er.z;
                     uint64_t exp = (1ull << 32) | 1ull;
                     if (er.w) cur = (uint64_t)(blu + 1u) << 32;  // the only parent: ready, no atomic
                     else
@@ -542,7 +653,14 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                         }
                         exp = obs;
                     }
-                    rdy = (uint32_t)cur == 0u;
+                    if ((uint32_t)cur == 0u) {
+                        const uint32_t wl0 = (uint32_t)(cur >> 32);
+                        if (r1 > r0) rdy = true;
+                        else {  // no out-edges: final here
+                            level[ww] = wl0;
+                            my_max = max(my_max, wl0);
+                        }
+                    }
                 }
                 const uint64_t rm = __ballot(rdy);
                 if (rm) {
@@ -552,46 +670,13 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                     if (lane == leader) b0 = atomicAdd(&ctl[(kShards + ps) * kCtlStride], (uint32_t)__popcll(rm));
                     b0 = __shfl(b0, (int)leader);
                     if (rdy)
-                        __hip_atomic_store(&Q[(size_t)ps * V + b0 + (uint32_t)__popcll(rm & lt)],
-                                           ((uint64_t)(pk ? (uint32_t)(cur >> 32) << 8 : (uint32_t)(cur >> 32)) << 32) |
-                                               ww,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        q_store(Q + ((size_t)ps * V + b0 + (uint32_t)__popcll(rm & lt)) * 2,
+                                q_ent(ww, (uint32_t)(cur >> 32), r0, r1));
                 }
             }
             if (lane == L) e = e1;  // the step below finishes (or continues) the item
         }
-        // per-lane step: up to kLaneEdges edges at once (loads and first CAS attempts all in
-        // flight together), so a chain link with a few fan-out children still takes one round
-        bool ready[kLaneEdges], fin_item = false, part = false;
-        bool jp[kHops - 1];        // a vertex passed by a jump has edges left: queue them (skip 1)
-        uint64_t jent[kHops - 1];
-#pragma unroll
-        for (uint32_t h = 0; h + 1 < kHops; ++h) { jp[h] = false; jent[h] = 0; }
-        uint64_t pent_part = 0;
-        uint32_t w[kLaneEdges], wl[kLaneEdges];
-#pragma unroll
-        for (uint32_t k = 0; k < kLaneEdges; ++k) ready[k] = false;
-        // the records of this round's edges are loaded first; the previous round's deferred
-        // pushes are stored after that, so waiting for their slot reservation (an atomic on a
-        // shared tail) overlaps the record load instead of preceding it -- on a chain the two
-        // were serial round trips per hop
-        const uint32_t ne = has_item ? min(e1 - e, kLaneEdges) : 0u;
-        uint4 erv[kLaneEdges], erh[kHops - 1];
-#pragma unroll
-        for (uint32_t k = 0; k < kLaneEdges; ++k)
-            if (k < ne) erv[k] = erec[e + k];
-#pragma unroll
-        for (uint32_t h = 0; h + 1 < kHops; ++h)  // the hops after edge e (k_edge_rec), same round trip
-            erh[h] = (pk && ne) ? erec2[(size_t)h * E + e] : make_uint4(0u, 0u, 0u, 0u);
-        if (npend) {
-            const uint32_t base = __shfl(pbase, 0);
-#pragma unroll
-            for (uint32_t k = 0; k < kPush; ++k)
-                if (pend[k]) __hip_atomic_store(&pq[base + pofs[k]], pent[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            npend = 0;
-        }
         if (has_item) {
-            uint32_t p0[kLaneEdges], p1[kLaneEdges];
             uint64_t cur[kLaneEdges], obs[kLaneEdges];
             bool only[kLaneEdges];
 #pragma unroll
@@ -629,23 +714,28 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                     }
                     if ((uint32_t)cur[k] == 0u) {
                         wl[k] = (uint32_t)(cur[k] >> 32);
-                        if (cw == FP_NONE) {
+                        if (p1[k] == p0[k]) {  // no out-edges: final here, nothing to queue
+                            level[w[k]] = wl[k];
+                            LVL_TR(wl[k]);
+                            my_max = max(my_max, wl[k]);
+                        } else if (cw == FP_NONE) {
                             cw = w[k]; cl = wl[k]; ce = p0[k]; ce1 = p1[k];
-                            // two-level jump: w ready through its only parent (this edge) and
-                            // its first dependent w2 ready through w alone -- w is final here,
-                            // the lane continues at w2, and w's other edges (if any) are queued
-                            // as a partial item skipping the first
-                            if (k == 0 && only[0] && pk) {
+                            // the jump: w ready through its only parent (this edge) and its first
+                            // dependent ready through w alone (and so on, kHops - 1 times) -- each
+                            // passed vertex is final here, the lane continues at the last one, and
+                            // the passed vertices' other edges are queued as partial items
+                            if (k == 0 && only[0]) {
                                 bool go = true;
 #pragma unroll
                                 for (uint32_t h = 0; h + 1 < kHops; ++h) {
                                     go = go && erh[h].w != 0u;
                                     if (go) {
                                         level[cw] = cl;
+                                        LVL_TR(cl);
                                         my_max = max(my_max, cl);
                                         if (ce + 1u < ce1) {
                                             jp[h] = true;
-                                            jent[h] = ((uint64_t)((cl << 8) | 1u) << 32) | cw;
+                                            jent[h] = q_ent(cw, cl, ce + 1u, ce1);
                                         }
                                         cw = erh[h].x; cl = cl + 1u; ce = erh[h].y; ce1 = erh[h].z;
                                     }
@@ -658,18 +748,19 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                 }
             }
             e += ne;
-            // a continuation with edges of u left: hand those to the queue as a partial
-            // item (entry level << 8 | edges to skip) and follow the chain now
-            if (cw != FP_NONE && e < e1 && pk && e - eb < 256u) {
+            // a continuation with edges of u left: hand those to the queue as a partial item
+            // and follow the chain now
+            if (cw != FP_NONE && e < e1) {
                 part = true;
-                pent_part = ((uint64_t)((lu << 8) | (e - eb)) << 32) | u;
+                pent_part = q_ent(u, lu, e, e1);
                 e = e1;
             }
             if (e >= e1) {
                 if (cw != FP_NONE) {  // continue down the chain in this lane
-                    u = cw; lu = cl; e = ce; e1 = ce1; eb = ce;
+                    u = cw; lu = cl; e = ce; e1 = ce1;
                     cw = FP_NONE;
                     level[u] = lu;
+                    LVL_TR(lu);
                     my_max = max(my_max, lu);
                 } else {
                     has_item = false;
@@ -677,34 +768,31 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
                 }
             }
         }
-        if (x != kQEmpty) {
+        if (x.lo != kQEmpty && x.hi != kQEmpty) {
             // the slot is consumed: empty it again, so that a clean finish leaves the queues empty
             // for the next call (kQClean)
-            __hip_atomic_store(const_cast<uint64_t *>(&q[slot]), kQEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            q_store(&q[2 * (size_t)slot], QEnt{kQEmpty, kQEmpty});
             has_claim = false;
             has_item = true;
-            u = (uint32_t)x;
-            const uint32_t hi = (uint32_t)(x >> 32);
-            lu = pk ? hi >> 8 : hi;
-            eb = row_ptr[u];
-            e = eb + (pk ? (hi & 255u) : 0u);
-            e1 = row_ptr[u + 1];
+            u = (uint32_t)x.lo;
+            lu = (uint32_t)(x.lo >> 32);
+            e = (uint32_t)(x.hi >> 32);
+            e1 = (uint32_t)x.hi;
             level[u] = lu;
+            LVL_TR(lu);
             my_max = max(my_max, lu);
         }
-        // claim one queue slot per lane without work (wave-aggregated); issued before the
-        // pushes so that its round trip overlaps theirs (the slot is first read next round)
+        // claim one queue slot per lane without work (wave-aggregated); the reservation is read
+        // next round, after that round's loads are issued, and the slot polled the round after
         {
-            const bool need = !has_claim && !has_item;
+            const bool need = !has_claim && !has_item && !cpend;
             const uint64_t nm = __ballot(need);
             if (nm) {
-                const uint32_t leader = (uint32_t)__builtin_ctzll(nm);
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(head, (uint32_t)__popcll(nm));
-                base = __shfl(base, (int)leader);
+                cleader = (uint32_t)__builtin_ctzll(nm);
+                if (lane == cleader) cbase = atomicAdd(head, (uint32_t)__popcll(nm));
                 if (need) {
-                    slot = base + (uint32_t)__popcll(nm & lt);
-                    has_claim = true;
+                    crank = (uint32_t)__popcll(nm & lt);
+                    cpend = true;
                 }
             }
         }
@@ -713,11 +801,11 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         // round trip overlaps the next round's loads instead of adding to this one
         // entries: [0, kLaneEdges) ready children, then the jumps' partial items, then u's part
         bool pp[kPush];
-        uint64_t pe[kPush];
+        QEnt pe[kPush];
 #pragma unroll
         for (uint32_t k = 0; k < kLaneEdges; ++k) {
             pp[k] = ready[k];
-            pe[k] = ((uint64_t)(pk ? wl[k] << 8 : wl[k]) << 32) | w[k];
+            pe[k] = q_ent(w[k], wl[k], p0[k], p1[k]);
         }
 #pragma unroll
         for (uint32_t h = 0; h + 1 < kHops; ++h) {
@@ -736,7 +824,7 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         if (tot) {
             const uint32_t ps = (sh + ++rr) % kShards;
             if (lane == 0) pbase = atomicAdd(&ctl[(kShards + ps) * kCtlStride], tot);
-            pq = Q + (size_t)ps * V;
+            pq = Q + (size_t)ps * V * 2;
             uint32_t run = 0;
 #pragma unroll
             for (uint32_t k = 0; k < kPush; ++k) {
@@ -747,6 +835,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             }
             npend = 1;
         }
+#ifdef FP_LVL_TRACE
+        if (trL0 != FP_NONE && trV > trT0) atomicMin(&g_lvl_trace[trL0], (unsigned long long)trT0);
+#endif
         const uint64_t fm = __ballot(fin_item);
         // relaxed, not waited for: this wave's push reservations (tail adds) have already
         // returned, and quiescence is decided on the counters alone
@@ -756,7 +847,7 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
             idle = 0;
             continue;
         }
-        // idle round: every lane holds a claim on an empty (or past-the-end) slot
+        // idle round: every lane holds a claim (or a reservation) on an empty (or past-the-end) slot
         uint32_t stop = 0;
         if (lane == 0) {
             if (monitor) {
@@ -778,11 +869,19 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint32_t *__restrict__ r
         }
         if (__shfl(stop, 0)) break;
         ++idle;
-        if (idle < 16) __builtin_amdgcn_s_sleep(1);
-        else __builtin_amdgcn_s_sleep(8);
+        if (idle < LVL_IDLE_SPIN) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(LVL_SLEEP_LONG);
     }
     for (int o = 32; o > 0; o >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor((int)my_max, o));
-    if (lane == 0 && my_max) atomicMax(&ctl[kMaxLevelWord], my_max);
+    // most waves never saw the top level: a load first keeps them off the one contended word (config 5:
+    // k_lvl_async -5 to -10 us, profiles/r07n_lvl_ab.txt)
+    if (lane == 0 && my_max && my_max > ag_ld32(&ctl[kMaxLevelWord])) atomicMax(&ctl[kMaxLevelWord], my_max);
+#ifdef FP_LVL_TRACE
+    if (lane == 0) {
+        atomicMin(&g_lvl_trace[4094], t_start);
+        atomicMax(&g_lvl_trace[4095], __builtin_amdgcn_s_memrealtime());
+    }
+#endif
 }
 
 // level -> sort keys; vertices never finished (cycle members and everything behind
@@ -1178,7 +1277,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         uint4 *erec2 = E ? (uint4 *)fp_ws_take(c, (size_t)E * 16 * (kHops - 1)) : nullptr;
         if (!state || !actl || (E && (!erec || !erec2))) return FP_ENOMEM;
         // the queues: the context's own buffer, emptied by the device only when dirty (kQClean)
-        const size_t qbytes = (size_t)V * 8 * kShards;
+        const size_t qbytes = (size_t)V * 16 * kShards;  // 16-B entries (k_lvl_async)
         if (qbytes + 256 > c->lvl_q_cap) {
             FP_HIP(hipStreamSynchronize(st));
             if (c->lvl_q) (void)hipFree(c->lvl_q);
@@ -1191,8 +1290,6 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         }
         uint64_t *Q = (uint64_t *)c->lvl_q;
         uint32_t *qflag = (uint32_t *)((char *)c->lvl_q + c->lvl_q_cap - 256);
-        // packed queue entries (level << 8 | edges to skip) need levels < 2^24: V < 2^24
-        const bool pk = V < (1u << 24);
         const unsigned zg = blocks_for((c->lvl_q_cap - 256) / 16, 256) < 8192 ? blocks_for((c->lvl_q_cap - 256) / 16, 256) : 8192;
         // "clean" covers the WHOLE buffer: a dirty buffer is refilled to its capacity, not to this
         // call's queue size, so a later call with a larger graph (a larger queue in the same
@@ -1224,17 +1321,22 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
         }
         const uint32_t vblocks = blocks_for(V, 256);
         const unsigned eg = E ? (blocks_for(E, 256) < 8192 ? blocks_for(E, 256) : 8192) : 0u;
-        k_lvl_prep<<<vblocks + eg, 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, g->col, V, E, vblocks, level, state, Q,
-                                                 actl, pk, erec, vrec, bad);
+        k_lvl_prep<<<vblocks + eg, 256, 0, st>>>(g->has_deps, indeg, g->row_ptr, g->col, V, E, vblocks, level, state,
+                                                 (uint4 *)Q, actl, erec, vrec, bad);
         FP_HIP(hipGetLastError());
         if (E) {
-            if (pk) {  // the hops are read only with packed queue entries
-                k_edge_hops<<<eg, 256, 0, st>>>(E, erec, erec2, bad);
-                FP_HIP(hipGetLastError());
+            k_edge_hops<<<eg, 256, 0, st>>>(E, erec, erec2, bad);
+            FP_HIP(hipGetLastError());
+#ifdef FP_LVL_TRACE
+            {
+                void *tr = nullptr;
+                FP_HIP(hipGetSymbolAddress(&tr, HIP_SYMBOL(g_lvl_trace)));
+                FP_HIP(hipMemsetAsync(tr, 0xFF, 4095 * 8, st));
+                FP_HIP(hipMemsetAsync((char *)tr + 4095 * 8, 0, 8, st));
             }
+#endif
             // one wave per block, kAsyncBlocks of them
-            k_lvl_async<<<kAsyncBlocks, 64, 0, st>>>(g->row_ptr, erec, erec2, E, V, state, Q, actl, level, c->d_err,
-                                                     pk, bad, qflag);
+            k_lvl_async<<<kAsyncBlocks, 64, 0, st>>>(erec, erec2, E, V, state, Q, actl, level, c->d_err, bad, qflag);
             FP_HIP(hipGetLastError());
         }
         // the cycle key (from the largest level seen) is computed on the device: no read-back; the

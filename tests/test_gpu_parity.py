@@ -173,8 +173,9 @@ def test_levelize_start_order_sort_limits(chain, sync, sort, planner, O):
 
 
 def test_levelize_async_unpacked_entries(planner, O):
-    """V >= 2^24: queue entries cannot pack (level << 8 | skip), so the asynchronous
-    levelizer runs without partial hand-off (fp_order.hip `pk`); same levels and order."""
+    """V >= 2^24: round 5 packed queue entries as (level << 8 | skip) and ran this size without
+    partial hand-off; the 16-B entries of round 6 carry the level and the edge range whole, so the
+    same path runs at every size.  Same levels and order as the oracle."""
     rng = np.random.default_rng(3)
     V = (1 << 24) + 100
     heads = rng.integers(0, V - 600, 40)
