@@ -923,7 +923,15 @@ __global__ void k_lvl_async_final(uint32_t V, const uint32_t *__restrict__ ctl, 
 // passes ping-pong (key, vertex) pairs through two scratch pairs.  The host enqueues the passes V
 // could need (ceil(bits(V + 1) / CS_BITS)) and reads nothing back: config 5's 509 levels take one
 // pass and the others return at once.
-constexpr uint32_t CS_TILE = 16384, CS_BITS = 10, CS_BINS = 1u << CS_BITS, CS_WAVES = 16, CS_MAX_TILES = 1024;
+// tiles of 16384 keys: config 5's 1M keys are 62 workgroups; 4096 / 8192 / 12288-key tiles ran
+// 0.693-0.699 / 0.653-0.656 / 0.651-0.660 ms against 0.653-0.656 (profiles/r07r_lvl_ab.txt)
+#ifndef CS_TILE_KEYS
+#define CS_TILE_KEYS 16384
+#endif
+#ifndef CS_REG_TILES
+#define CS_REG_TILES 64
+#endif
+constexpr uint32_t CS_TILE = CS_TILE_KEYS, CS_BITS = 10, CS_BINS = 1u << CS_BITS, CS_WAVES = 16, CS_MAX_TILES = 1024;
 
 struct CsPass {
     uint32_t sh, nb, nbits;  // digit shift, bins (digits < nb), bits the match masks test
@@ -941,6 +949,12 @@ __device__ __forceinline__ CsPass cs_pass_k(uint32_t p, uint32_t kmax) {
     return c;
 }
 __device__ __forceinline__ CsPass cs_pass(uint32_t p, const uint32_t *ck) { return cs_pass_k(p, *ck); }
+// the error word and the key range in one round trip (a pass that is not needed returns after it)
+__device__ __forceinline__ bool cs_start(const uint32_t *bad, const uint32_t *ck, uint32_t &kmax) {
+    const uint32_t b = *bad;
+    kmax = *ck;
+    return b == 0u;
+}
 // The asynchronous levelizer sorts its levels in place of keys (LvlMap): pass 0 reads level[] and
 // sorts a CYCLE vertex (FP_NONE) under the cycle key, max(largest level, 1) + 1, which k_cs_hist
 // derives from the schedule's largest level and publishes for the later kernels (no key array
@@ -957,15 +971,15 @@ __device__ __forceinline__ uint32_t cs_digit(uint32_t key, const CsPass &c) {
 __global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t p,
                                                   uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
                                                   uint32_t *__restrict__ hist, LvlMap lm) {
-    if (*bad) return;
     const bool map = lm.maxl && p == 0;
+    const uint32_t badv = *bad, maxl = map ? *lm.maxl : 0u, ckv = map ? 0u : *ck;  // one round trip
+    if (badv) return;
     uint32_t ckey = 0;
     if (map) {
-        const uint32_t maxl = *lm.maxl;
         ckey = (maxl > 1 ? maxl : 1u) + 1u;
         if (blockIdx.x == 0 && threadIdx.x == 0) *ck = ckey;  // the later kernels read it
     }
-    const CsPass c = map ? cs_pass_k(p, ckey) : cs_pass(p, ck);
+    const CsPass c = cs_pass_k(p, map ? ckey : ckv);
     if (!c.active) return;
     __shared__ uint32_t h[CS_BINS];
     for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) h[b] = 0;
@@ -993,13 +1007,14 @@ __global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ k
 
 __global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t p, const uint32_t *__restrict__ ck,
                           const uint32_t *__restrict__ bad) {
-    if (*bad) return;
-    const CsPass c = cs_pass(p, ck);
+    uint32_t kmax;
+    if (!cs_start(bad, ck, kmax)) return;
+    const CsPass c = cs_pass_k(p, kmax);
     if (!c.active) return;
     const uint32_t nb = c.nb;
     __shared__ uint32_t tot[CS_BINS];
     const uint32_t b = threadIdx.x;  // one bin per thread (nb <= CS_BINS = blockDim)
-    constexpr uint32_t REG_TILES = 64;  // up to 1M keys: the bin's counts stay in registers
+    constexpr uint32_t REG_TILES = CS_REG_TILES;  // up to 1M keys: the bin's counts stay in registers
     uint32_t x[REG_TILES];
     uint32_t run = 0;
     const bool in_regs = ntiles <= REG_TILES;
@@ -1065,10 +1080,11 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ bad, const uint32_t *__restrict__ off,
                                                      uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
                                                      uint32_t *__restrict__ vout, bool map) {
-    if (*bad) return;
+    uint32_t kmax;
+    if (!cs_start(bad, ck, kmax)) return;
     map = map && p == 0;  // levels as keys (LvlMap): *ck is the cycle key, written by k_cs_hist
-    const uint32_t ckey = map ? *ck : 0u;
-    const CsPass c = cs_pass(p, ck);
+    const uint32_t ckey = map ? kmax : 0u;
+    const CsPass c = cs_pass_k(p, kmax);
     if (!c.active) return;
     const uint32_t nb = c.nb;
     __shared__ uint32_t wh[CS_WAVES][CS_BINS];
