@@ -109,11 +109,14 @@ def test_levelize_async_shapes(shape, planner, O):
     assert np.array_equal(level, el) and np.array_equal(order, eo) and ncyc == en
 
 
-@pytest.mark.parametrize("shape", ["ring_with_tails", "join_then_chain", "random_forest", "cycle_fed_tree"])
+@pytest.mark.parametrize("shape", ["ring_with_tails", "join_then_chain", "random_forest", "cycle_fed_tree",
+                                   "chain_big_side_fans"])
 def test_levelize_only_parent_shapes(shape, planner, O):
     """Only-parent structures for k_lvl_async's chain hops: rings of only-parent edges with chains
-    hanging off them (never final), a deep chain below a join, a 200k-vertex random forest, and a
-    tree fed by a cycle member."""
+    hanging off them (never final), a deep chain below a join, a 200k-vertex random forest, a
+    tree fed by a cycle member, and a chain whose vertices pass on 300-2000 side edges each as
+    partial items (round 5 capped a partial's skip at 256 edges; 16-B entries carry any range),
+    half of the side children leaves (final where they become ready, never queued)."""
     rng = np.random.default_rng(11)
     if shape == "ring_with_tails":
         V = 20_000
@@ -130,6 +133,13 @@ def test_levelize_only_parent_shapes(shape, planner, O):
         par = (rng.random(V - 1) * np.arange(1, V)).astype(np.int64)  # parent < child: a forest
         edges = list(zip(par.tolist(), range(1, V)))
         edges += [(int(a), int(b)) for a, b in zip(rng.integers(0, V // 2, 2000), rng.integers(V // 2, V, 2000)) if a < b]
+    elif shape == "chain_big_side_fans":
+        V = 60_000
+        edges = [(v, v + 1) for v in range(0, 3000)]                  # first edges: the chain
+        for v in range(0, 3000, 97):                                  # hop vertices with big fans
+            fan = int(rng.integers(300, 2000))
+            edges += [(v, int(t)) for t in rng.integers(3001, V, fan)]
+        edges += [(int(a), int(b)) for a, b in zip(rng.integers(3001, 30_000, 20_000), rng.integers(30_000, V, 20_000))]
     else:
         V = 9_000
         edges = [(0, 1), (1, 2), (2, 0), (3, 0)]                      # 0 has two parents (3 and 2)
