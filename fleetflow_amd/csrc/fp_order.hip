@@ -239,12 +239,14 @@ constexpr uint32_t kPush = kLaneEdges + kHops;  // queue entries a lane may push
 // lane, so spreading the items over more waves shortens the rounds of the lanes on the long chains,
 // until idle waves' queue polls start to cost more
 constexpr uint32_t kAsyncBlocks = 2048;
+constexpr uint32_t kInitClaims = kAsyncBlocks / kShards * 64u;  // slots per shard claimed at the start
 #ifndef LVL_SLEEP_LONG
 #define LVL_SLEEP_LONG 8  // s_sleep of an idle wave after LVL_IDLE_SPIN short (s_sleep 1) rounds (2 / 32: +-1 %, r07k)
 #endif
 #ifndef LVL_IDLE_SPIN
 #define LVL_IDLE_SPIN 16
 #endif
+
 // ctl layout (u32 index, S = kShards): head[s] = s*32, tail[s] = (S+s)*32, done[s] = (2S+s)*32,
 // fin = 3S*32, abort = (3S+1)*32, maxlvl = (3S+2)*32
 constexpr uint32_t kCtlWords = kMaxLevelWord + kCtlStride;
@@ -313,7 +315,9 @@ __global__ void k_lvl_zero(uint32_t V, uint32_t *__restrict__ indeg, uint32_t *_
     const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
     for (size_t i = i0; i < V; i += st) indeg[i] = 0u;
     if (i0 < 16) ncyc[i0] = 0u;
-    for (size_t i = i0; i < kCtlWords; i += st) actl[i] = 0u;
+    // the claim heads start past the slots every wave holds from its start (k_lvl_async)
+    for (size_t i = i0; i < kCtlWords; i += st)
+        actl[i] = i < kShards * kCtlStride && i % kCtlStride == 0 ? kInitClaims : 0u;
     if (i0 == 0 && ncyc_out) *ncyc_out = 0u;
     if (*qflag != kQClean)
         for (size_t i = i0; i < q4; i += st) Q4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -549,8 +553,12 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
     const uint64_t lt = (1ull << lane) - 1ull;
     // lane state: a claim on a queue slot, or an item u (level lu) with edges [e, e1),
     // and at most one continuation cw (level cl, edges [ce, ce1))
-    bool has_claim = false, has_item = false;
-    uint32_t slot = 0, u = 0, lu = 0, e = 0, e1 = 0, my_max = 0, idle = 0;
+    // every lane starts with a claim: wave k of a shard holds its slots [64k, 64k + 64) (the heads
+    // start at kInitClaims, k_lvl_zero), so the first items are polled in the first round (config 5:
+    // 0.641-0.656 against 0.650-0.663 ms, profiles/r07u_lvl_ab.txt; raising a chain-walking wave's
+    // s_setprio to 1 / 3 cost 8-13 us, r07v_lvl_ab.txt)
+    bool has_claim = true, has_item = false;
+    uint32_t slot = (blockIdx.x / kShards) * 64u + lane, u = 0, lu = 0, e = 0, e1 = 0, my_max = 0, idle = 0;
     uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     // deferred pushes (see below): entries, offsets, the reserved base (lane 0)
