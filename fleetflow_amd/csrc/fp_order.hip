@@ -536,6 +536,15 @@ __device__ __forceinline__ void q_store(uint64_t *slot2, const QEnt &x) {
     __hip_atomic_store(slot2, x.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The pushes of one round: entries, per-lane offsets, the target queue, the reservation's result
+// (lane 0) and the items the round finished (their done count follows the entries' stores).
+struct PushSet {
+    bool pend[kPush];
+    uint32_t pofs[kPush];
+    QEnt pent[kPush];
+    uint32_t tot, ps, pbase, ndone;
+};
+
 __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec, const uint4 *__restrict__ erec2,
                                                   uint32_t E, uint32_t V, uint64_t *__restrict__ state,
                                                   uint64_t *__restrict__ Q, uint32_t *__restrict__ ctl,
@@ -561,14 +570,18 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
     uint32_t slot = (blockIdx.x / kShards) * 64u + lane, u = 0, lu = 0, e = 0, e1 = 0, my_max = 0, idle = 0;
     uint32_t cw = FP_NONE, cl = 0, ce = 0, ce1 = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    // deferred pushes (see below): entries, offsets, the reserved base (lane 0)
-    bool pend[kPush];
-    uint32_t pofs[kPush], pbase = 0, npend = 0;
-    QEnt pent[kPush];
-    uint64_t *pq = Q;
-    // deferred claims: the reservation's result (leader lane), the leader, this lane's rank
-    bool cpend = false;
+    // two push sets, alternating by round parity (see the loop comment)
+    PushSet sA, sB;
+#pragma unroll
+    for (uint32_t k = 0; k < kPush; ++k) sA.pend[k] = sB.pend[k] = false;
+    sA.tot = sB.tot = sA.ndone = sB.ndone = 0;
+    sA.ps = sB.ps = sA.pbase = sB.pbase = 0;
+    // claims: needed (issued next round), reserved (read the round after), the leader, this lane's rank
+    bool cneed = false, cpend = false;
     uint32_t cbase = 0, cleader = 0, crank = 0;
+    // a consumed queue slot, emptied next round
+    bool rs_pend = false;
+    uint32_t rs_slot = 0;
 #ifdef FP_LVL_TRACE
     uint32_t trL = FP_NONE;
     uint64_t trT = 0;
@@ -577,13 +590,18 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
     // to save a round trip per join level on the chain: k_lvl_async 495 -> 540 us on config 5,
     // profiles/r07h_lvl_prefetch_kernel_stats.csv -- the extra loads of every join edge cost more than they saved.)
     //
-    // A round issues everything it will wait for first -- the edge records, then the polls of
-    // claimed slots -- and only then waits: for the previous round's push and claim reservations,
-    // the cooperative expansions and the records.  A wave's memory operations complete in order, so
-    // any dependent load issued later in the round (round 5 loaded a claimed item's row_ptr pair,
-    // then the next round's records behind it) stalls every lane of the wave, the lanes walking
-    // chains included.
-    while (true) {
+    // A wave's memory operations complete in order (loads, stores and atomics on one counter), so a
+    // round's wait for its edge records is also a wait for every store and atomic issued before
+    // them.  A round therefore issues its records and polls first and only then the previous rounds'
+    // deferred work: the queue stores of the pushes reserved one round ago (set SP), the
+    // reservation of the pushes computed last round (set SQ), the done count of the items whose
+    // pushes were just stored, the emptying of consumed slots, and the claims.  Every store and
+    // atomic thus has a whole round to complete before a load waits behind it.  (Round 5 stored its
+    // pushes right behind the reservation's return: a chain lane's round waited for the previous
+    // round's queue stores, 2.3 -> 5.3 us per 4-level round on config 5 in the trace build.)
+    // Ordering for termination: the done count of an item is issued only after the reservation of
+    // its children's slots has returned (the wait on SP.pbase), so done never overtakes tail.
+    auto round = [&](PushSet &SP, PushSet &SQ) -> bool {
         // a vertex with many edges left (a chain head feeding a whole fan-out layer) is expanded by
         // the whole wave, 64 edges per step (below); the others take one edge step per lane
         const bool coop = has_item && e1 - e >= kCoopEdges;
@@ -618,20 +636,42 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
             x.lo = ag_ld64(&q[2 * (size_t)slot]);
             x.hi = ag_ld64(&q[2 * (size_t)slot + 1]);
         }
-        // the previous round's reservations: pushes stored, claims become slots (polled next round)
-        if (npend) {
-            const uint32_t base = __shfl(pbase, 0);
+        // ---- the deferred work, behind this round's loads
+        if (SP.tot) {  // reserved at the previous round's top: store the entries
+            const uint32_t base = __shfl(SP.pbase, 0);
+            uint64_t *pq = Q + (size_t)SP.ps * V * 2;
 #pragma unroll
             for (uint32_t k = 0; k < kPush; ++k)
-                if (pend[k]) q_store(pq + 2 * (size_t)(base + pofs[k]), pent[k]);
-            npend = 0;
+                if (SP.pend[k]) q_store(pq + 2 * (size_t)(base + SP.pofs[k]), SP.pent[k]);
+            SP.tot = 0;
         }
-        if (__ballot(cpend)) {
+        if (SP.ndone) {  // their items are done (relaxed, not waited for)
+            if (lane == 0) __hip_atomic_fetch_add(done, SP.ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            SP.ndone = 0;
+        }
+        if (SQ.tot && lane == 0) SQ.pbase = atomicAdd(&ctl[(kShards + SQ.ps) * kCtlStride], SQ.tot);
+        if (rs_pend) {  // the slot consumed last round: empty again (a clean finish leaves the queues empty)
+            q_store(&q[2 * (size_t)rs_slot], QEnt{kQEmpty, kQEmpty});
+            rs_pend = false;
+        }
+        if (__ballot(cpend)) {  // last round's claim reservation: the slot is polled next round
             const uint32_t b = __shfl(cbase, (int)cleader);
             if (cpend) {
                 slot = b + crank;
                 has_claim = true;
                 cpend = false;
+            }
+        }
+        {  // claim one queue slot per lane without work (wave-aggregated)
+            const uint64_t nm = __ballot(cneed);
+            if (nm) {
+                cleader = (uint32_t)__builtin_ctzll(nm);
+                if (lane == cleader) cbase = atomicAdd(head, (uint32_t)__popcll(nm));
+                if (cneed) {
+                    crank = (uint32_t)__popcll(nm & lt);
+                    cpend = true;
+                    cneed = false;
+                }
             }
         }
         while (bm) {
@@ -670,6 +710,8 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
                         }
                     }
                 }
+                // these pushes are stored at once, after their reservation returns: the items
+                // they finish are counted in a later round, behind the stores
                 const uint64_t rm = __ballot(rdy);
                 if (rm) {
                     const uint32_t leader = (uint32_t)__builtin_ctzll(rm);
@@ -742,7 +784,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
                                         LVL_TR(cl);
                                         my_max = max(my_max, cl);
                                         if (ce + 1u < ce1) {
+#ifndef LVL_DROP_JP  // diagnostics only: wrong levels, times the chain walk without its side pushes
                                             jp[h] = true;
+#endif
                                             jent[h] = q_ent(cw, cl, ce + 1u, ce1);
                                         }
                                         cw = erh[h].x; cl = cl + 1u; ce = erh[h].y; ce1 = erh[h].z;
@@ -759,7 +803,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
             // a continuation with edges of u left: hand those to the queue as a partial item
             // and follow the chain now
             if (cw != FP_NONE && e < e1) {
+#ifndef LVL_DROP_JP
                 part = true;
+#endif
                 pent_part = q_ent(u, lu, e, e1);
                 e = e1;
             }
@@ -776,10 +822,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
                 }
             }
         }
-        if (x.lo != kQEmpty && x.hi != kQEmpty) {
-            // the slot is consumed: empty it again, so that a clean finish leaves the queues empty
-            // for the next call (kQClean)
-            q_store(&q[2 * (size_t)slot], QEnt{kQEmpty, kQEmpty});
+        if (x.lo != kQEmpty && x.hi != kQEmpty) {  // a claimed item arrived
+            rs_pend = true;
+            rs_slot = slot;
             has_claim = false;
             has_item = true;
             u = (uint32_t)x.lo;
@@ -790,24 +835,9 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
             LVL_TR(lu);
             my_max = max(my_max, lu);
         }
-        // claim one queue slot per lane without work (wave-aggregated); the reservation is read
-        // next round, after that round's loads are issued, and the slot polled the round after
-        {
-            const bool need = !has_claim && !has_item && !cpend;
-            const uint64_t nm = __ballot(need);
-            if (nm) {
-                cleader = (uint32_t)__builtin_ctzll(nm);
-                if (lane == cleader) cbase = atomicAdd(head, (uint32_t)__popcll(nm));
-                if (need) {
-                    crank = (uint32_t)__popcll(nm & lt);
-                    cpend = true;
-                }
-            }
-        }
-        // pushes, deferred by one round: this round reserves the queue slots (the add's
-        // result is not waited for), the next round stores the entries -- the reservation's
-        // round trip overlaps the next round's loads instead of adding to this one
-        // entries: [0, kLaneEdges) ready children, then the jumps' partial items, then u's part
+        cneed = !has_claim && !has_item && !cpend;
+        // this round's pushes into SP: reserved next round (as that round's SQ), stored the round
+        // after; entries: [0, kLaneEdges) ready children, then the jumps' partial items, then u's part
         bool pp[kPush];
         QEnt pe[kPush];
 #pragma unroll
@@ -829,33 +859,29 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
             rm[k] = __ballot(pp[k]);
             tot += (uint32_t)__popcll(rm[k]);
         }
+        SP.tot = tot;
         if (tot) {
-            const uint32_t ps = (sh + ++rr) % kShards;
-            if (lane == 0) pbase = atomicAdd(&ctl[(kShards + ps) * kCtlStride], tot);
-            pq = Q + (size_t)ps * V * 2;
+            SP.ps = (sh + ++rr) % kShards;
             uint32_t run = 0;
 #pragma unroll
             for (uint32_t k = 0; k < kPush; ++k) {
-                pend[k] = pp[k];
-                pofs[k] = run + (uint32_t)__popcll(rm[k] & lt);
-                pent[k] = pe[k];
+                SP.pend[k] = pp[k];
+                SP.pofs[k] = run + (uint32_t)__popcll(rm[k] & lt);
+                SP.pent[k] = pe[k];
                 run += (uint32_t)__popcll(rm[k]);
             }
-            npend = 1;
         }
+        SP.ndone = (uint32_t)__popcll(__ballot(fin_item));
 #ifdef FP_LVL_TRACE
         if (trL0 != FP_NONE && trV > trT0) atomicMin(&g_lvl_trace[trL0], (unsigned long long)trT0);
 #endif
-        const uint64_t fm = __ballot(fin_item);
-        // relaxed, not waited for: this wave's push reservations (tail adds) have already
-        // returned, and quiescence is decided on the counters alone
-        if (fm && lane == (uint32_t)__builtin_ctzll(fm))
-            __hip_atomic_fetch_add(done, (uint32_t)__popcll(fm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__ballot(has_item) || fm || npend) {
+        // busy while anything is in hand or deferred
+        if (__ballot(has_item || rs_pend) || SP.tot || SP.ndone || SQ.tot || SQ.ndone) {
             idle = 0;
-            continue;
+            return false;
         }
-        // idle round: every lane holds a claim (or a reservation) on an empty (or past-the-end) slot
+        // idle round: every lane holds a claim (or a reservation) on an empty (or past-the-end)
+        // slot, and nothing is deferred
         uint32_t stop = 0;
         if (lane == 0) {
             if (monitor) {
@@ -875,10 +901,17 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
                 stop = 1;
             }
         }
-        if (__shfl(stop, 0)) break;
+        if (__shfl(stop, 0)) return true;
         ++idle;
         if (idle < LVL_IDLE_SPIN) __builtin_amdgcn_s_sleep(1);
         else __builtin_amdgcn_s_sleep(LVL_SLEEP_LONG);
+        return false;
+    };
+    // rounds alternate the sets: a round stores SP (reserved in the round before), reserves SQ
+    // (computed in the round before) and computes its own pushes into SP
+    while (true) {
+        if (round(sA, sB)) break;
+        if (round(sB, sA)) break;
     }
     for (int o = 32; o > 0; o >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor((int)my_max, o));
     // most waves never saw the top level: a load first keeps them off the one contended word (config 5:
