@@ -1009,11 +1009,33 @@ __device__ __forceinline__ uint32_t cs_digit(uint32_t key, const CsPass &c) {
     return min(c.last ? key >> c.sh : (key >> c.sh) & (CS_BINS - 1u), c.nb - 1u);
 }
 
+__device__ __forceinline__ uint64_t cs_match(uint32_t v, bool valid, uint32_t nbits) {
+    uint64_t m = __builtin_amdgcn_ballot_w64(valid);
+    for (uint32_t i = 0; i < nbits; ++i) {
+        const bool bit = (v >> i) & 1u;
+        const uint64_t bb = __builtin_amdgcn_ballot_w64(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
 __global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t p,
                                                   uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
                                                   uint32_t *__restrict__ hist, LvlMap lm) {
     const bool map = lm.maxl && p == 0;
-    const uint32_t badv = *bad, maxl = map ? *lm.maxl : 0u, ckv = map ? 0u : *ck;  // one round trip
+    // the tile's keys are loaded with the control words, all in one round trip (a load per
+    // iteration behind the LDS atomics cost a round trip each: 15.5 us for config 5's 1M keys)
+    constexpr uint32_t PER = CS_TILE / 1024u;
+    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
+    uint32_t kv[PER];
+    auto load = [&]() {
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) {
+            const size_t i = t0 + threadIdx.x + j * 1024u;
+            kv[j] = i < V ? keys[i] : 0u;
+        }
+    };
+    if (p == 0) load();  // pass 0 always runs; a later pass may not be needed (loaded below)
+    const uint32_t badv = *bad, maxl = map ? *lm.maxl : 0u, ckv = map ? 0u : *ck;
     if (badv) return;
     uint32_t ckey = 0;
     if (map) {
@@ -1022,18 +1044,26 @@ __global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ k
     }
     const CsPass c = cs_pass_k(p, map ? ckey : ckv);
     if (!c.active) return;
+    if (p != 0) load();
     __shared__ uint32_t h[CS_BINS];
     for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) h[b] = 0;
     __syncthreads();
-    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
     uint32_t ncy = 0;
-    for (uint32_t i = threadIdx.x; i < CS_TILE && t0 + i < V; i += blockDim.x) {
-        uint32_t k = keys[t0 + i];
+    const uint32_t wbase = threadIdx.x & ~63u;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        if (t0 + wbase + j * 1024u >= V) break;  // wave-uniform
+        const bool valid = t0 + threadIdx.x + j * 1024u < V;
+        uint32_t k = kv[j];
         if (map) {
-            ncy += k == FP_NONE ? 1u : 0u;
+            ncy += valid && k == FP_NONE ? 1u : 0u;
             k = cs_key(k, ckey);
         }
-        atomicAdd(&h[cs_digit(k, c)], 1u);
+        const uint32_t d = valid ? cs_digit(k, c) : 0u;
+        // (counting equal digits once per wave by their match masks instead: hist 12.1 -> 17.6 us,
+        // scatter 16.8 -> 25.3 us on config 5, profiles/r08a_lvl_ab.txt -- the ballots cost more than
+        // the LDS conflicts they avoid)
+        if (valid) atomicAdd(&h[d], 1u);
     }
     if (map) {  // the cycle vertices: one atomic per wave that has any
         for (int o = 32; o > 0; o >>= 1) ncy += (uint32_t)__shfl_xor((int)ncy, o);
@@ -1104,15 +1134,6 @@ __global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t
     }
 }
 
-__device__ __forceinline__ uint64_t cs_match(uint32_t v, bool valid, uint32_t nbits) {
-    uint64_t m = __builtin_amdgcn_ballot_w64(valid);
-    for (uint32_t i = 0; i < nbits; ++i) {
-        const bool bit = (v >> i) & 1u;
-        const uint64_t bb = __builtin_amdgcn_ballot_w64(bit);
-        m &= bit ? bb : ~bb;
-    }
-    return m;
-}
 
 // pass p: (keys, vals) -> (kout, vout), or the vertices alone -> order on the last pass.
 // vals null: the vertex is the key's index (pass 0).
@@ -1121,24 +1142,40 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ bad, const uint32_t *__restrict__ off,
                                                      uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
                                                      uint32_t *__restrict__ vout, bool map) {
+    // the wave's slice of keys (and vertices) is loaded once, with the control words, and kept in
+    // registers for both walks (a load per iteration cost a round trip each: 23.4 us for config 5)
+    constexpr uint32_t slice = CS_TILE / CS_WAVES, PER = slice / 64u;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const size_t s0 = (size_t)blockIdx.x * CS_TILE + (size_t)w * slice;
+    uint32_t kv[PER], xv[PER];
+    auto load = [&]() {
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) {
+            const size_t v = s0 + j * 64u + lane;
+            kv[j] = v < V ? keys[v] : 0u;
+            xv[j] = v < V ? (vals ? vals[v] : (uint32_t)v) : 0u;
+        }
+    };
+    if (p == 0) load();  // pass 0 always runs; a later pass may not be needed (loaded below)
     uint32_t kmax;
     if (!cs_start(bad, ck, kmax)) return;
     map = map && p == 0;  // levels as keys (LvlMap): *ck is the cycle key, written by k_cs_hist
     const uint32_t ckey = map ? kmax : 0u;
     const CsPass c = cs_pass_k(p, kmax);
     if (!c.active) return;
+    if (p != 0) load();
     const uint32_t nb = c.nb;
     __shared__ uint32_t wh[CS_WAVES][CS_BINS];
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
     for (uint32_t i = t; i < CS_WAVES * CS_BINS; i += blockDim.x) (&wh[0][0])[i] = 0;
     __syncthreads();
-    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
-    const uint32_t slice = CS_TILE / CS_WAVES;
-    const size_t s0 = t0 + (size_t)w * slice;
-    for (uint32_t i = lane; i < slice && s0 + i < V; i += 64) {
-        const uint32_t k = keys[s0 + i];
-        atomicAdd(&wh[w][cs_digit(map ? cs_key(k, ckey) : k, c)], 1u);
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        if (s0 + j * 64u >= V) break;  // wave-uniform
+        const bool valid = s0 + j * 64u + lane < V;
+        if (map) kv[j] = cs_key(kv[j], ckey);
+        const uint32_t d = valid ? cs_digit(kv[j], c) : 0u;
+        if (valid) atomicAdd(&wh[w][d], 1u);
     }
     __syncthreads();
     for (uint32_t b = t; b < nb; b += blockDim.x) {  // per bin: wave offsets in wave order
@@ -1150,12 +1187,13 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
         }
     }
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < slice && s0 + i0 < V; i0 += 64) {
-        const size_t v = s0 + i0 + lane;
-        const bool valid = i0 + lane < slice && v < V;
-        const uint32_t key = valid ? (map ? cs_key(keys[v], ckey) : keys[v]) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        if (s0 + j * 64u >= V) break;  // wave-uniform
+        const bool valid = s0 + j * 64u + lane < V;
+        const uint32_t key = kv[j];  // (mapped above)
         const uint32_t k = valid ? cs_digit(key, c) : 0u;
-        const uint32_t x = valid ? (vals ? vals[v] : (uint32_t)v) : 0u;
+        const uint32_t x = xv[j];
         const uint64_t m = cs_match(k, valid, c.nbits);
         const uint32_t o = wh[w][k];
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane's read before the update
