@@ -15,6 +15,13 @@
 
 int fp_hip_fail(hipError_t e);
 
+// A word that only gains bits (the batch OR words of the packed-record decision, fp_pipe_pk.h): the
+// atomic only when this block adds a bit.  Most blocks find every bit set already, and atomics on one
+// word serialise: config 4 issued 2 per scenario block from each of three kernels.
+__device__ __forceinline__ void fp_or_new_bits(uint32_t *w, uint32_t bits) {
+    if (bits & ~*(volatile uint32_t *)w) atomicOr(w, bits);
+}
+
 struct fp_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;

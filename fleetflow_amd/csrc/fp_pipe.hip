@@ -1156,8 +1156,8 @@ __global__ __launch_bounds__(256) void k_node_summary(uint32_t N, const uint32_t
             summ[(size_t)blockIdx.x * 4 + 1] = a;
         }
         if (RANGE) {
-            if (oc) atomicOr(&rng[0], oc);
-            if (om) atomicOr(&rng[1], om);
+            fp_or_new_bits(&rng[0], oc);
+            fp_or_new_bits(&rng[1], om);
         }
     }
 }

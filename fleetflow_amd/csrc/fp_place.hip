@@ -192,8 +192,8 @@ __global__ __launch_bounds__(256) void k_make_keys(const uint32_t *__restrict__ 
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (red[0]) atomicOr(&rng[0], red[0]);
-        if (red[1]) atomicOr(&rng[1], red[1]);
+        fp_or_new_bits(&rng[0], red[0]);
+        fp_or_new_bits(&rng[1], red[1]);
     }
 }
 
@@ -443,8 +443,8 @@ __device__ void ss_generic(const ScenSortArgs &a, uint16_t *X, uint16_t *WH, uin
     }
     __syncthreads();
     if (t == 0) {
-        atomicOr(&a.rng[0], HS[0]);
-        atomicOr(&a.rng[1], HS[1]);
+        fp_or_new_bits(&a.rng[0], HS[0]);
+        fp_or_new_bits(&a.rng[1], HS[1]);
     }
 }
 
@@ -810,8 +810,8 @@ __global__ __launch_bounds__(1024) void k_scen_sort(const ScenSortArgs a) {
             om |= (uint32_t)__shfl_xor((int)om, o);
         }
         if (lane == 0) {
-            atomicOr(&a.rng[0], oc);
-            atomicOr(&a.rng[1], om);
+            fp_or_new_bits(&a.rng[0], oc);
+            fp_or_new_bits(&a.rng[1], om);
         }
     }
 }
