@@ -596,9 +596,10 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
     // deferred work: the queue stores of the pushes reserved one round ago (set SP), the
     // reservation of the pushes computed last round (set SQ), the done count of the items whose
     // pushes were just stored, the emptying of consumed slots, and the claims.  Every store and
-    // atomic thus has a whole round to complete before a load waits behind it.  (Round 5 stored its
-    // pushes right behind the reservation's return: a chain lane's round waited for the previous
-    // round's queue stores, 2.3 -> 5.3 us per 4-level round on config 5 in the trace build.)
+    // atomic thus has a whole round to complete before a load waits behind it.  (Config 5, trace
+    // build: a chain's 4-level round took 5.3 us with its side pushes and 2.3 us with them dropped,
+    // profiles/r07w_*; this order brought it to 4.0-4.3 us, r07x_trace.jsonl, and the production
+    // kernel 3-6 us, r07x_lvl_ab.txt.)
     // Ordering for termination: the done count of an item is issued only after the reservation of
     // its children's slots has returned (the wait on SP.pbase), so done never overtakes tail.
     auto round = [&](PushSet &SP, PushSet &SQ) -> bool {
