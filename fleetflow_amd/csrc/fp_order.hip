@@ -974,6 +974,7 @@ __global__ void k_lvl_async_final(uint32_t V, const uint32_t *__restrict__ ctl, 
 #define CS_REG_TILES 64
 #endif
 constexpr uint32_t CS_TILE = CS_TILE_KEYS, CS_BITS = 10, CS_BINS = 1u << CS_BITS, CS_WAVES = 16, CS_MAX_TILES = 1024;
+constexpr uint32_t kCsPassesMax = (32 + CS_BITS - 1) / CS_BITS;  // passes a 32-bit key can need
 
 struct CsPass {
     uint32_t sh, nb, nbits;  // digit shift, bins (digits < nb), bits the match masks test
@@ -1019,37 +1020,14 @@ __device__ __forceinline__ uint64_t cs_match(uint32_t v, bool valid, uint32_t nb
     }
     return m;
 }
-__global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t p,
-                                                  uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
-                                                  uint32_t *__restrict__ hist, LvlMap lm) {
-    const bool map = lm.maxl && p == 0;
-    // the tile's keys are loaded with the control words, all in one round trip (a load per
-    // iteration behind the LDS atomics cost a round trip each: 15.5 us for config 5's 1M keys)
-    constexpr uint32_t PER = CS_TILE / 1024u;
-    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
-    uint32_t kv[PER];
-    auto load = [&]() {
-#pragma unroll
-        for (uint32_t j = 0; j < PER; ++j) {
-            const size_t i = t0 + threadIdx.x + j * 1024u;
-            kv[j] = i < V ? keys[i] : 0u;
-        }
-    };
-    if (p == 0) load();  // pass 0 always runs; a later pass may not be needed (loaded below)
-    const uint32_t badv = *bad, maxl = map ? *lm.maxl : 0u, ckv = map ? 0u : *ck;
-    if (badv) return;
-    uint32_t ckey = 0;
-    if (map) {
-        ckey = (maxl > 1 ? maxl : 1u) + 1u;
-        if (blockIdx.x == 0 && threadIdx.x == 0) *ck = ckey;  // the later kernels read it
-    }
-    const CsPass c = cs_pass_k(p, map ? ckey : ckv);
-    if (!c.active) return;
-    if (p != 0) load();
+// the tile's histogram of the pass digit (LDS) -> its row of hist (keys already loaded: kv[j] is
+// key t0 + threadIdx.x + 1024 j); map: levels as keys, counting the cycle vertices
+template <uint32_t PER>
+__device__ __forceinline__ void cs_hist_tile(const uint32_t (&kv)[PER], size_t t0, uint32_t V, const CsPass &c,
+                                             bool map, uint32_t ckey, uint32_t *__restrict__ row, uint32_t &ncy) {
     __shared__ uint32_t h[CS_BINS];
     for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) h[b] = 0;
     __syncthreads();
-    uint32_t ncy = 0;
     const uint32_t wbase = threadIdx.x & ~63u;
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {
@@ -1066,24 +1044,12 @@ __global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ k
         // the LDS conflicts they avoid)
         if (valid) atomicAdd(&h[d], 1u);
     }
-    if (map) {  // the cycle vertices: one atomic per wave that has any
-        for (int o = 32; o > 0; o >>= 1) ncy += (uint32_t)__shfl_xor((int)ncy, o);
-        if ((threadIdx.x & 63) == 0 && ncy) {
-            atomicAdd(lm.ncyc, ncy);
-            if (lm.ncyc_out) atomicAdd(lm.ncyc_out, ncy);
-        }
-    }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) hist[(size_t)blockIdx.x * c.nb + b] = h[b];
+    for (uint32_t b = threadIdx.x; b < c.nb; b += blockDim.x) row[b] = h[b];
 }
 
-__global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t p, const uint32_t *__restrict__ ck,
-                          const uint32_t *__restrict__ bad) {
-    uint32_t kmax;
-    if (!cs_start(bad, ck, kmax)) return;
-    const CsPass c = cs_pass_k(p, kmax);
-    if (!c.active) return;
-    const uint32_t nb = c.nb;
+// one workgroup of CS_BINS threads: hist[tile][bin] <- bin base + keys of the bin in earlier tiles
+__device__ __forceinline__ void cs_scan_bins(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t nb) {
     __shared__ uint32_t tot[CS_BINS];
     const uint32_t b = threadIdx.x;  // one bin per thread (nb <= CS_BINS = blockDim)
     constexpr uint32_t REG_TILES = CS_REG_TILES;  // up to 1M keys: the bin's counts stay in registers
@@ -1135,52 +1101,27 @@ __global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t
     }
 }
 
-
-// pass p: (keys, vals) -> (kout, vout), or the vertices alone -> order on the last pass.
-// vals null: the vertex is the key's index (pass 0).
-__global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
-                                                     uint32_t V, uint32_t p, const uint32_t *__restrict__ ck,
-                                                     const uint32_t *__restrict__ bad, const uint32_t *__restrict__ off,
-                                                     uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
-                                                     uint32_t *__restrict__ vout, bool map) {
-    // the wave's slice of keys (and vertices) is loaded once, with the control words, and kept in
-    // registers for both walks (a load per iteration cost a round trip each: 23.4 us for config 5)
-    constexpr uint32_t slice = CS_TILE / CS_WAVES, PER = slice / 64u;
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const size_t s0 = (size_t)blockIdx.x * CS_TILE + (size_t)w * slice;
-    uint32_t kv[PER], xv[PER];
-    auto load = [&]() {
-#pragma unroll
-        for (uint32_t j = 0; j < PER; ++j) {
-            const size_t v = s0 + j * 64u + lane;
-            kv[j] = v < V ? keys[v] : 0u;
-            xv[j] = v < V ? (vals ? vals[v] : (uint32_t)v) : 0u;
-        }
-    };
-    if (p == 0) load();  // pass 0 always runs; a later pass may not be needed (loaded below)
-    uint32_t kmax;
-    if (!cs_start(bad, ck, kmax)) return;
-    map = map && p == 0;  // levels as keys (LvlMap): *ck is the cycle key, written by k_cs_hist
-    const uint32_t ckey = map ? kmax : 0u;
-    const CsPass c = cs_pass_k(p, kmax);
-    if (!c.active) return;
-    if (p != 0) load();
-    const uint32_t nb = c.nb;
+// a wave's slice of the tile in (key, vertex) order of the pass digit: per-wave counts, the wave
+// offsets from the tile's row of the scanned hist, then ranks by ballot match masks (kv already
+// mapped by the caller when map; kv[j], xv[j] = key / vertex s0 + 64 j + lane)
+template <uint32_t PER>
+__device__ __forceinline__ void cs_scatter_slice(const uint32_t (&kv)[PER], const uint32_t (&xv)[PER], size_t s0,
+                                                 uint32_t V, const CsPass &c, const uint32_t *__restrict__ offrow,
+                                                 uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
+                                                 uint32_t *__restrict__ vout) {
     __shared__ uint32_t wh[CS_WAVES][CS_BINS];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, nb = c.nb;
     const uint64_t lt = (1ull << lane) - 1ull;
     for (uint32_t i = t; i < CS_WAVES * CS_BINS; i += blockDim.x) (&wh[0][0])[i] = 0;
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {
         if (s0 + j * 64u >= V) break;  // wave-uniform
-        const bool valid = s0 + j * 64u + lane < V;
-        if (map) kv[j] = cs_key(kv[j], ckey);
-        const uint32_t d = valid ? cs_digit(kv[j], c) : 0u;
-        if (valid) atomicAdd(&wh[w][d], 1u);
+        if (s0 + j * 64u + lane < V) atomicAdd(&wh[w][cs_digit(kv[j], c)], 1u);
     }
     __syncthreads();
     for (uint32_t b = t; b < nb; b += blockDim.x) {  // per bin: wave offsets in wave order
-        uint32_t run = off[(size_t)blockIdx.x * nb + b];
+        uint32_t run = offrow[b];
         for (uint32_t ww = 0; ww < CS_WAVES; ++ww) {
             const uint32_t x = wh[ww][b];
             wh[ww][b] = run;
@@ -1192,7 +1133,7 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
     for (uint32_t j = 0; j < PER; ++j) {
         if (s0 + j * 64u >= V) break;  // wave-uniform
         const bool valid = s0 + j * 64u + lane < V;
-        const uint32_t key = kv[j];  // (mapped above)
+        const uint32_t key = kv[j];
         const uint32_t k = valid ? cs_digit(key, c) : 0u;
         const uint32_t x = xv[j];
         const uint64_t m = cs_match(k, valid, c.nbits);
@@ -1210,6 +1151,155 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
+}
+
+constexpr uint32_t CS_HPER = CS_TILE / 1024u;               // keys per thread in a tile's histogram
+constexpr uint32_t CS_SLICE = CS_TILE / CS_WAVES, CS_SPER = CS_SLICE / 64u;  // per wave / lane in the scatter
+
+__global__ __launch_bounds__(1024) void k_cs_hist(const uint32_t *__restrict__ keys, uint32_t V, uint32_t p,
+                                                  uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
+                                                  uint32_t *__restrict__ hist, LvlMap lm, uint32_t *__restrict__ bar) {
+    const bool map = lm.maxl && p == 0;
+    // the tile's keys are loaded with the control words, all in one round trip (a load per
+    // iteration behind the LDS atomics cost a round trip each: 15.5 us for config 5's 1M keys)
+    const size_t t0 = (size_t)blockIdx.x * CS_TILE;
+    uint32_t kv[CS_HPER];
+    auto load = [&]() {
+#pragma unroll
+        for (uint32_t j = 0; j < CS_HPER; ++j) {
+            const size_t i = t0 + threadIdx.x + j * 1024u;
+            kv[j] = i < V ? keys[i] : 0u;
+        }
+    };
+    if (p == 0) load();  // pass 0 always runs; a later pass may not be needed (loaded below)
+    const uint32_t badv = *bad, maxl = map ? *lm.maxl : 0u, ckv = map ? 0u : *ck;
+    if (badv) return;
+    uint32_t ckey = 0;
+    if (map) {
+        ckey = (maxl > 1 ? maxl : 1u) + 1u;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *ck = ckey;  // the later kernels read it
+    }
+    // pass 0 clears the barrier words of the later passes' single-launch kernel (k_cs_pass_late)
+    if (p == 0 && bar && blockIdx.x == 0 && threadIdx.x < 2 * kCsPassesMax) bar[threadIdx.x] = 0u;
+    const CsPass c = cs_pass_k(p, map ? ckey : ckv);
+    if (!c.active) return;
+    if (p != 0) load();
+    uint32_t ncy = 0;
+    cs_hist_tile(kv, t0, V, c, map, ckey, hist + (size_t)blockIdx.x * c.nb, ncy);
+    if (map) {  // the cycle vertices: one atomic per wave that has any
+        for (int o = 32; o > 0; o >>= 1) ncy += (uint32_t)__shfl_xor((int)ncy, o);
+        if ((threadIdx.x & 63) == 0 && ncy) {
+            atomicAdd(lm.ncyc, ncy);
+            if (lm.ncyc_out) atomicAdd(lm.ncyc_out, ncy);
+        }
+    }
+}
+
+__global__ void k_cs_scan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t p, const uint32_t *__restrict__ ck,
+                          const uint32_t *__restrict__ bad) {
+    uint32_t kmax;
+    if (!cs_start(bad, ck, kmax)) return;
+    const CsPass c = cs_pass_k(p, kmax);
+    if (!c.active) return;
+    cs_scan_bins(hist, ntiles, c.nb);
+}
+
+// pass p: (keys, vals) -> (kout, vout), or the vertices alone -> order on the last pass.
+// vals null: the vertex is the key's index (pass 0).
+__global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                     uint32_t V, uint32_t p, const uint32_t *__restrict__ ck,
+                                                     const uint32_t *__restrict__ bad, const uint32_t *__restrict__ off,
+                                                     uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
+                                                     uint32_t *__restrict__ vout, bool map) {
+    // the wave's slice of keys (and vertices) is loaded once, with the control words, and kept in
+    // registers for both walks (a load per iteration cost a round trip each: 23.4 us for config 5)
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t s0 = (size_t)blockIdx.x * CS_TILE + (size_t)w * CS_SLICE;
+    uint32_t kv[CS_SPER], xv[CS_SPER];
+    auto load = [&]() {
+#pragma unroll
+        for (uint32_t j = 0; j < CS_SPER; ++j) {
+            const size_t v = s0 + j * 64u + lane;
+            kv[j] = v < V ? keys[v] : 0u;
+            xv[j] = v < V ? (vals ? vals[v] : (uint32_t)v) : 0u;
+        }
+    };
+    if (p == 0) load();  // pass 0 always runs; a later pass may not be needed (loaded below)
+    uint32_t kmax;
+    if (!cs_start(bad, ck, kmax)) return;
+    map = map && p == 0;  // levels as keys (LvlMap): *ck is the cycle key, written by k_cs_hist
+    const CsPass c = cs_pass_k(p, kmax);
+    if (!c.active) return;
+    if (p != 0) load();
+    if (map) {
+#pragma unroll
+        for (uint32_t j = 0; j < CS_SPER; ++j) kv[j] = cs_key(kv[j], kmax);
+    }
+    cs_scatter_slice(kv, xv, s0, V, c, off + (size_t)blockIdx.x * c.nb, order, kout, vout);
+}
+
+// A pass after the first in ONE launch when its tiles fit one workgroup per CU (ntiles <=
+// CS_FUSED_TILES): the histogram, the scan (workgroup 0) and the scatter meet at two grid barriers.
+// A pass the keys do not need returns after one round trip: config 5's second pass (509 levels, but
+// V = 1M could need 20 bits) cost three launches that return at once, 16 us.  The barriers give up
+// after 10 s (FP_EDEVICE) so that a grid that is not all resident cannot hang the device.
+constexpr uint32_t CS_FUSED_TILES = 64;
+__device__ __forceinline__ bool cs_grid_sync(uint32_t *cnt, uint32_t target, uint32_t *err) {
+    __shared__ uint32_t ok;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // this workgroup's writes before its arrival
+        atomicAdd(cnt, 1u);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t good = 1;
+        while (ag_ld32(cnt) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100ull * 1000 * 1000 * 10) {
+                atomicMax(err, (uint32_t)(-FP_EDEVICE));
+                good = 0;
+                break;
+            }
+        }
+        __threadfence();  // the others' writes after their arrival
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0u;
+}
+__global__ __launch_bounds__(1024) void k_cs_pass_late(const uint32_t *__restrict__ keys,
+                                                       const uint32_t *__restrict__ vals, uint32_t V, uint32_t p,
+                                                       const uint32_t *__restrict__ ck, const uint32_t *__restrict__ bad,
+                                                       uint32_t *__restrict__ hist, uint32_t ntiles,
+                                                       uint32_t *__restrict__ order, uint32_t *__restrict__ kout,
+                                                       uint32_t *__restrict__ vout, uint32_t *__restrict__ bar,
+                                                       uint32_t *__restrict__ err) {
+    uint32_t kmax;
+    if (!cs_start(bad, ck, kmax)) return;
+    const CsPass c = cs_pass_k(p, kmax);
+    if (!c.active) return;
+    {
+        const size_t t0 = (size_t)blockIdx.x * CS_TILE;
+        uint32_t kv[CS_HPER], ncy = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < CS_HPER; ++j) {
+            const size_t i = t0 + threadIdx.x + j * 1024u;
+            kv[j] = i < V ? keys[i] : 0u;
+        }
+        cs_hist_tile(kv, t0, V, c, false, 0u, hist + (size_t)blockIdx.x * c.nb, ncy);
+    }
+    if (!cs_grid_sync(&bar[2 * p], gridDim.x, err)) return;
+    if (blockIdx.x == 0) cs_scan_bins(hist, ntiles, c.nb);
+    if (!cs_grid_sync(&bar[2 * p + 1], gridDim.x, err)) return;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t s0 = (size_t)blockIdx.x * CS_TILE + (size_t)w * CS_SLICE;
+    uint32_t kv[CS_SPER], xv[CS_SPER];
+#pragma unroll
+    for (uint32_t j = 0; j < CS_SPER; ++j) {
+        const size_t v = s0 + j * 64u + lane;
+        kv[j] = v < V ? keys[v] : 0u;
+        xv[j] = v < V ? vals[v] : 0u;
+    }
+    cs_scatter_slice(kv, xv, s0, V, c, hist + (size_t)blockIdx.x * c.nb, order, kout, vout);
 }
 
 // ---- small graphs: the whole levelization in one workgroup ---------------------------------
@@ -1279,18 +1369,29 @@ int fp_dev_legacy_order_impl(fp_ctx *c, const fp_graph *g, uint32_t *perm) {
 // above when its tiles cover V, else (or with FP_OPT_LEVEL_SORT = 0) rocprim's radix sort over all
 // 32 key bits (vals = the identity, k_lvl_*final).  No read-back either way.  Scratch: two
 // (key, vertex) pairs, kb[0]/vb[0] and kb[1]/vb[1].
+#ifndef CS_FUSE_LATE
+#define CS_FUSE_LATE 1  // passes after the first in one launch (k_cs_pass_late) when the tiles allow
+#endif
 static int level_sort(hipStream_t st, bool counting, uint32_t *keys, uint32_t *const kb[2], uint32_t *const vb[2],
                       uint32_t *order, uint32_t V, uint32_t *ck, const uint32_t *bad, void *tmp,
-                      size_t sort_tmp, uint32_t *cs_hist, LvlMap lm = LvlMap{nullptr, nullptr, nullptr}) {
+                      size_t sort_tmp, uint32_t *cs_hist, uint32_t *err,
+                      LvlMap lm = LvlMap{nullptr, nullptr, nullptr}) {
     const uint32_t ntiles = (uint32_t)(((size_t)V + CS_TILE - 1) / CS_TILE);
     if (counting && ntiles <= CS_MAX_TILES) {
         // the largest key either schedule can produce: the async cycle key is max(level, 1) + 1 <=
         // V + 1; the level-synchronous one is iters + 2 <= (V + 1) + 2: V + 3
         const uint32_t passes = (fp_bitwidth((uint64_t)V + 3) + CS_BITS - 1) / CS_BITS;
+        uint32_t *bar = cs_hist + (size_t)CS_MAX_TILES * CS_BINS;  // the late passes' barrier words
         for (uint32_t p = 0; p < passes; ++p) {
             const uint32_t *ik = p ? kb[(p - 1) & 1] : keys;
             const uint32_t *iv = p ? vb[(p - 1) & 1] : nullptr;
-            k_cs_hist<<<ntiles, 1024, 0, st>>>(ik, V, p, ck, bad, cs_hist, lm);
+            if (CS_FUSE_LATE && p && ntiles <= CS_FUSED_TILES) {
+                k_cs_pass_late<<<ntiles, 1024, 0, st>>>(ik, iv, V, p, ck, bad, cs_hist, ntiles, order, kb[p & 1],
+                                                        vb[p & 1], bar, err);
+                FP_HIP(hipGetLastError());
+                continue;
+            }
+            k_cs_hist<<<ntiles, 1024, 0, st>>>(ik, V, p, ck, bad, cs_hist, lm, bar);
             FP_HIP(hipGetLastError());
             k_cs_scan<<<1, CS_BINS, 0, st>>>(cs_hist, ntiles, p, ck, bad);
             FP_HIP(hipGetLastError());
@@ -1342,7 +1443,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     const bool binned_indeg = !level_sync && E && bin_b <= kBinMaxB && fp_opt(c, FP_OPT_INDEG_BIN, 1) != 0;
     const size_t bin_ws = binned_indeg ? (size_t)E * 4 + (size_t)(bin_b + 1) * bin_nwg * 4 + (size_t)V * 16 + 768 : 0;
     const size_t async_ws = level_sync ? 0 : (size_t)V * 8 + (size_t)E * 16 * kHops + kCtlWords * 4 + bin_ws;
-    const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 : 0;
+    const size_t cs_ws = counting ? (size_t)CS_MAX_TILES * CS_BINS * 4 + 256 : 0;  // + the barrier words
     int rc = fp_ws_reserve(c, (size_t)V * 4 * 6 + ncnt * 4 + sort_tmp + async_ws + cs_ws + 23 * 256);
     if (rc) return rc;
     fp_ws_reset(c);
@@ -1442,11 +1543,11 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
             // the counting sort reads the levels themselves (LvlMap): cycle key, keys and cycle count
             // come out of its first pass
             const LvlMap lm{actl + kMaxLevelWord, ncyc, n_cycle_dev};
-            if ((rc = level_sort(st, counting, level, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist, lm))) return rc;
+            if ((rc = level_sort(st, counting, level, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist, c->d_err, lm))) return rc;
         } else {
             k_lvl_async_final<<<blocks_for(V, 256), 256, 0, st>>>(V, actl, level, keys, vals, ncyc, ck, bad, n_cycle_dev);
             FP_HIP(hipGetLastError());
-            if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
+            if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist, c->d_err))) return rc;
         }
         fp_prof_end(c, FP_K_LEVEL, ev);
         return FP_OK;
@@ -1495,7 +1596,7 @@ int fp_dev_levelize_impl(fp_ctx *c, const fp_graph *g, uint32_t *level, uint32_t
     const uint32_t cyc_key = iters + 2;
     k_lvl_final<<<blocks_for(V, 256), 256, 0, st>>>(indeg, V, cyc_key, level, keys, vals, ncyc, ck);
     FP_HIP(hipGetLastError());
-    if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist))) return rc;
+    if ((rc = level_sort(st, counting, keys, kb, vb, order, V, ck, bad, tmp, sort_tmp, cs_hist, c->d_err))) return rc;
     if (n_cycle_dev) FP_HIP(hipMemcpyAsync(n_cycle_dev, ncyc, 4, hipMemcpyDeviceToDevice, st));
     fp_prof_end(c, FP_K_LEVEL, ev);
     return FP_OK;
