@@ -1050,7 +1050,7 @@ __device__ __forceinline__ void cs_hist_tile(const uint32_t (&kv)[PER], size_t t
 
 // one workgroup of CS_BINS threads: hist[tile][bin] <- bin base + keys of the bin in earlier tiles
 __device__ __forceinline__ void cs_scan_bins(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t nb) {
-    __shared__ uint32_t tot[CS_BINS];
+    __shared__ uint32_t tot[CS_BINS / 64];  // the waves' sums
     const uint32_t b = threadIdx.x;  // one bin per thread (nb <= CS_BINS = blockDim)
     constexpr uint32_t REG_TILES = CS_REG_TILES;  // up to 1M keys: the bin's counts stay in registers
     uint32_t x[REG_TILES];
@@ -1080,16 +1080,20 @@ __device__ __forceinline__ void cs_scan_bins(uint32_t *__restrict__ hist, uint32
             }
         }
     }
-    tot[b] = b < nb ? run : 0u;
-    __syncthreads();
-    // exclusive scan of tot[] (Hillis-Steele in LDS)
-    for (uint32_t o = 1; o < CS_BINS; o <<= 1) {
-        const uint32_t y = b >= o ? tot[b - o] : 0u;
-        __syncthreads();
-        tot[b] += y;
-        __syncthreads();
+    // exclusive scan of the bin totals: within each wave by shuffles, then the earlier waves' sums
+    // (one barrier; the LDS Hillis-Steele scan took twenty)
+    const uint32_t lane = b & 63, wv = b >> 6;
+    uint32_t inc = b < nb ? run : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if ((int)lane >= o) inc += y;
     }
-    const uint32_t base = tot[b] - run;  // inclusive - own
+    if (lane == 63) tot[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t q = 0; q < wv; ++q) pre += tot[q];
+    const uint32_t base = pre + inc - (b < nb ? run : 0u);
     if (b < nb) {
         if (in_regs) {
 #pragma unroll
