@@ -1244,6 +1244,8 @@ __global__ __launch_bounds__(1024) void k_cs_scatter(const uint32_t *__restrict_
 
 // A pass after the first in ONE launch when its tiles fit one workgroup per CU (ntiles <=
 // CS_FUSED_TILES): the histogram, the scan (workgroup 0) and the scatter meet at two grid barriers.
+// (The first pass, which always runs, is faster as three launches: 39.6 us fused against 12.8 + 7.0 +
+// 17.0 us on config 5, profiles/r08g_lvl_ab.txt -- the other workgroups wait through the scan.)
 // A pass the keys do not need returns after one round trip: config 5's second pass (509 levels, but
 // V = 1M could need 20 bits) cost three launches that return at once, 16 us.  The barriers give up
 // after 10 s (FP_EDEVICE) so that a grid that is not all resident cannot hang the device.
