@@ -633,6 +633,8 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
 #endif
         // the poll of a claimed slot, behind the records
         QEnt x{kQEmpty, kQEmpty};
+        // (polling the first word alone, and the second once the first is set, halves the poll
+        // loads but delays every pickup by a round: config 5 +17 us, profiles/r08k_lvl_ab.txt)
         if (has_claim && slot < V) {
             x.lo = ag_ld64(&q[2 * (size_t)slot]);
             x.hi = ag_ld64(&q[2 * (size_t)slot + 1]);
@@ -788,7 +790,11 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
 #ifndef LVL_DROP_JP  // diagnostics only: wrong levels, times the chain walk without its side pushes
                                             jp[h] = true;
 #endif
+#ifdef LVL_SKIP_SIDE  // diagnostics only: side items are taken and dropped (wrong levels)
+                                            jent[h] = q_ent(cw, cl | 0x80000000u, ce + 1u, ce1);
+#else
                                             jent[h] = q_ent(cw, cl, ce + 1u, ce1);
+#endif
                                         }
                                         cw = erh[h].x; cl = cl + 1u; ce = erh[h].y; ce1 = erh[h].z;
                                     }
@@ -807,7 +813,11 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
 #ifndef LVL_DROP_JP
                 part = true;
 #endif
+#ifdef LVL_SKIP_SIDE
+                pent_part = q_ent(u, lu | 0x80000000u, e, e1);
+#else
                 pent_part = q_ent(u, lu, e, e1);
+#endif
                 e = e1;
             }
             if (e >= e1) {
@@ -823,6 +833,15 @@ __global__ __launch_bounds__(64) void k_lvl_async(const uint4 *__restrict__ erec
                 }
             }
         }
+#ifdef LVL_SKIP_SIDE
+        if (x.lo != kQEmpty && x.hi != kQEmpty && (x.lo >> 63)) {
+            rs_pend = true;
+            rs_slot = slot;
+            has_claim = false;
+            fin_item = true;
+            x.lo = kQEmpty;
+        }
+#endif
         if (x.lo != kQEmpty && x.hi != kQEmpty) {  // a claimed item arrived
             rs_pend = true;
             rs_slot = slot;
