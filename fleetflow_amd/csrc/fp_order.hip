@@ -238,7 +238,10 @@ constexpr uint32_t kPush = kLaneEdges + kHops;  // queue entries a lane may push
 // 8192 0.81, 256 0.92; profiles/r04v_lvl_grid_ab.txt) -- a wave round lasts as long as its slowest
 // lane, so spreading the items over more waves shortens the rounds of the lanes on the long chains,
 // until idle waves' queue polls start to cost more
-constexpr uint32_t kAsyncBlocks = 2048;
+#ifndef LVL_BLOCKS  // round 6 at 16-B entries: 1024 / 1536 / 3072 blocks 0.647-0.650 / 0.633 / 0.636-0.640
+#define LVL_BLOCKS 2048  // against 0.624-0.629 ms (profiles/r08o_lvl_ab.txt)
+#endif
+constexpr uint32_t kAsyncBlocks = LVL_BLOCKS;
 constexpr uint32_t kInitClaims = kAsyncBlocks / kShards * 64u;  // slots per shard claimed at the start
 #ifndef LVL_SLEEP_LONG
 #define LVL_SLEEP_LONG 8  // s_sleep of an idle wave after LVL_IDLE_SPIN short (s_sleep 1) rounds (2 / 32: +-1 %, r07k)
