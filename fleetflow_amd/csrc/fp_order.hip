@@ -224,7 +224,10 @@ constexpr uint64_t kQEmpty = ~0ull;
 // edges left at which the wave expands a vertex together, and edges a lane relaxes per round
 // (config 5: 16 / 1 0.775 ms; cooperative at 8 0.823, at 32 0.779; 2 edges per lane 0.877;
 // profiles/r04aa_lvl_tuning_ab.txt)
-constexpr uint32_t kCoopEdges = 16;
+#ifndef LVL_COOP_EDGES  // round 6: 8 / 32 edges 0.670-0.674 / 0.621-0.626 against 0.623-0.626 ms; 16 queues
+#define LVL_COOP_EDGES 16  // 0.633-0.638 (profiles/r08p_lvl_ab.txt)
+#endif
+constexpr uint32_t kCoopEdges = LVL_COOP_EDGES;
 constexpr uint32_t kLaneEdges = 1;
 // levels a lane may jump per round along only-parent first edges: 4 (config 5 0.84 ms; 6 hops 0.86, 8 hops
 // 0.92 -- more records to build and load per round, profiles/r04m_lvl_hops_ab.txt; round 6 at 16-B queue
