@@ -61,6 +61,8 @@ DAG5 = (1000, 500, 50, 10_000, 333)  # chains, chain length, fan-out layers, lay
 FLAGS = 7
 HBM_PEAK_GBPS = 8000.0
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
+# config 5a's HBM bytes per levelize call (tools/lvl_pmc.sh + tools/summarize_lvl_pmc.py)
+PMC_LVL_FILE = os.path.join(ROOT, "profiles", "pmc_levelize_latest.json")
 MODEL_FILE = os.path.join(ROOT, "profiles", "pipe_model_latest.json")
 
 
@@ -478,13 +480,19 @@ def levelize_leg(planner, dev, steps):
               "unit": "vertices/s", "perm": perm_t.cpu().numpy().view(np.uint32)}
     nbytes = 16 * V + 12 * E + 4
     levels = level_t.cpu().numpy().view(np.uint32)
+    pmc = _load_json(PMC_LVL_FILE) or {}
+    traffic = pmc.get("hbm_bytes_per_call")
     out = {"workload": "BASELINE config 5a: levelize the 1M-vertex depends_on DAG (deep chains + wide fan-out, "
                        "333 3-cycles)", "V": V, "E": E, "value": (V + E) / step_s, "unit": "(V+E)/s",
            "ms_per_step": step_s * 1e3, "steps": steps, "kernel_ms": kernel_s * 1e3,
            "levels": int(levels[levels != 0xFFFFFFFF].max()) + 1, "cycle_vertices": int(ncyc_t.item()),
            "roofline": {"bound": "hbm", "kernel": "levelizer (k_indeg + k_lvl_async + level sort, fp_order.hip)",
                         "achieved": nbytes / kernel_s / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": nbytes / kernel_s / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                        "frac": nbytes / kernel_s / 1e9 / HBM_PEAK_GBPS, "traffic": traffic,
+                        "traffic_over_essential": traffic / nbytes if traffic else None,
+                        "traffic_source": (f"rocprofv3 PMC {pmc.get('tag')}: 2 x FETCH_SIZE + WRITE_SIZE summed over "
+                                           "the call's kernels, separate passes (profiles/pmc_levelize_latest.json)")
+                        if traffic else None,
                         "algorithmic_bytes": nbytes,
                         "limiter": "latency of the longest dependency chain (500 levels of chains)"}}
     return out, (rp, col, hd), level_t, (levels, order_t.cpu().numpy().view(np.uint32), int(ncyc_t.item())), legacy
