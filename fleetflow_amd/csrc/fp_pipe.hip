@@ -297,6 +297,15 @@ constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
 constexpr uint32_t SYS_MAX_G = 4;
 // ... and the packed one (fp_pipe_pk.h) for stages of at most this many (its records take one VGPR
 // fewer per group)
+// Bucket-mask upkeep (UPD in fpp_groups): clearing a touched node's bucket bits after each group's
+// queue keeps the masks tight, but with the packed records a check costs less than the upkeep: off,
+// the masks stay as the stage built them (a stale mask is a superset, so the plans are the same --
+// identical digests), and config 4's FFD went 12.16 -> 11.18 ms, 2048 / 1024 / 512 scenarios 8.79 ->
+// 7.92, 6.91 -> 6.23, 5.63 -> 4.98 ms (profiles/r08vw_mask_upkeep_ab.jsonl).  Round 2 measured the
+// opposite for its u32 20-group stages (57 vs 66 ms).  1 turns it back on.
+#ifndef FPP_MASK_UPKEEP
+#define FPP_MASK_UPKEEP 0
+#endif
 #ifndef FPP_PK_SYS_MAX_G
 #define FPP_PK_SYS_MAX_G 4
 #endif
@@ -843,7 +852,7 @@ k_ffd_pipe(const PipeArgs a_arg) {
             unsigned long long gst[4] = {0, 0, 0, 0};  // diagnostics: check-loop / bookkeeping cycles, queues, touched
             if (prio == 1u && todo) __builtin_amdgcn_s_setprio(FP_PRIO_LEVEL);
             if (todo)
-                fpp_groups<G, (G > 1), (BLK == 64 || (FPP_IB1024 && G > SYS_MAX_G)) && FPP_IB, PK>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
+                fpp_groups<G, (G > 1) && FPP_MASK_UPKEEP, (BLK == 64 || (FPP_IB1024 && G > SYS_MAX_G)) && FPP_IB, PK>(std::make_integer_sequence<uint32_t, G>{}, nxt, placed, my_assign, usedbits,
                                        used_hi, rcf, rmf, rcu, rlab, cpu, mem, req, conf, (uint32_t)cand,
                                        (uint32_t)((uint64_t)cand >> 32), my_t, lane, Mw, mlane,
                                        __builtin_amdgcn_readfirstlane(gbase * 64u), qc, qm, nchk, nhit, a.sys, gst,
