@@ -285,7 +285,10 @@ using RecT = uint32_t[G];
 // Corner-node limit of the prefilter, by stage width (r03m A/B, profiles/r03m_ab*.jsonl): narrow
 // (<= 4-group) stages 4 -- config 3 65.3 -> 64.1 ms (16: 65.3, 32: 70.8); wide stages off -- config
 // 4 17.54 -> 17.28 ms (4: 17.48, 32: 17.96).
-constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = 0;
+#ifndef FPP_PF_MAX_WIDE  // without the mask upkeep too: 4 / 16 corner nodes in the wide stages, config 4
+#define FPP_PF_MAX_WIDE 0  // 11.98-12.01 against 11.20-11.31 ms (profiles/r08y_prefilter_wide_ab.jsonl)
+#endif
+constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = FPP_PF_MAX_WIDE;
 // lane selects by inverse ballot in the one-wave kernels' group bookkeeping (fpp_lane_sel)
 #ifndef FPP_IB
 #define FPP_IB 1
