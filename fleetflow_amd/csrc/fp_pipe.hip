@@ -293,9 +293,9 @@ constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = FPP_PF_MAX_WIDE;
 #ifndef FPP_IB
 #define FPP_IB 1
 #endif
-#ifndef FPP_IB1024  // ... and in the 1024-thread kernels of more than SYS_MAX_G groups: off, slower there
-#define FPP_IB1024 0  // (512 / 1024 scenarios 6.43 / 7.79 vs 6.21 / 7.58 ms, profiles/r05n_ib1024_ab.jsonl)
-#endif
+#ifndef FPP_IB1024  // ... and in the 1024-thread kernels of more than SYS_MAX_G groups: on since the mask
+#define FPP_IB1024 1  // upkeep went (512 / 1024 scenarios 4.91-4.97 / 6.15-6.20 vs 4.96-5.01 / 6.19-6.31 ms,
+#endif                // profiles/r08z_ib1024_ab.jsonl; with the upkeep round 5 measured 6.43 / 7.79 vs 6.21 / 7.58)
 // the systolic group fill (fp_pipe_sys.h) is compiled for stages of at most this many groups
 constexpr uint32_t SYS_MAX_G = 4;
 // ... and the packed one (fp_pipe_pk.h) for stages of at most this many (its records take one VGPR
