@@ -288,7 +288,10 @@ using RecT = uint32_t[G];
 #ifndef FPP_PF_MAX_WIDE  // without the mask upkeep too: 4 / 16 corner nodes in the wide stages, config 4
 #define FPP_PF_MAX_WIDE 0  // 11.98-12.01 against 11.20-11.31 ms (profiles/r08y_prefilter_wide_ab.jsonl)
 #endif
-constexpr uint32_t PF_MAX_NARROW = 4, PF_MAX_WIDE = FPP_PF_MAX_WIDE;
+#ifndef FPP_PF_MAX_NARROW
+#define FPP_PF_MAX_NARROW 4
+#endif
+constexpr uint32_t PF_MAX_NARROW = FPP_PF_MAX_NARROW, PF_MAX_WIDE = FPP_PF_MAX_WIDE;
 // lane selects by inverse ballot in the one-wave kernels' group bookkeeping (fpp_lane_sel)
 #ifndef FPP_IB
 #define FPP_IB 1
