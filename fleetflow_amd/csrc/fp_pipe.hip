@@ -1892,8 +1892,11 @@ int fp_pipe_launch(fp_ctx *c, uint32_t S, uint32_t C, uint32_t N, uint32_t scen_
     // later) are batched: FP_OPT_LINK_PUBLISH full slots per head store and vmcnt(0) drain.  A
     // bounded ring publishes every slot: its producer may wait on the consumer's tail, which
     // moves only on published slots.
+    // Default: 32 slots at 4096 scenarios and more, 8 below -- at 2048 / 1024 scenarios the
+    // consumer phase starts sooner (7.70-7.74 / 6.01-6.03 against 7.91-7.92 / 6.11-6.24 ms), at 4096
+    // 8 is +0.3 % (profiles/r09h_link_publish_sweep.jsonl).
     {
-        const int64_t pv = fp_opt(c, FP_OPT_LINK_PUBLISH, 32);
+        const int64_t pv = fp_opt(c, FP_OPT_LINK_PUBLISH, S >= 4096 ? 32 : 8);
         a.publish = geo.bounded ? 1u : (uint32_t)(pv < 1 ? 1 : pv > 1024 ? 1024 : pv);
         uint32_t p2 = 1;
         while (p2 * 2 <= a.publish) p2 *= 2;
