@@ -231,7 +231,8 @@ constexpr uint32_t kCoopEdges = LVL_COOP_EDGES;
 constexpr uint32_t kLaneEdges = 1;
 // levels a lane may jump per round along only-parent first edges: 4 (config 5 0.84 ms; 6 hops 0.86, 8 hops
 // 0.92 -- more records to build and load per round, profiles/r04m_lvl_hops_ab.txt; round 6 at 16-B queue
-// entries: 4 / 6 / 8 hops 0.663-0.665 / 0.664-0.665 / 0.738 ms, profiles/r07p_lvl_ab.txt)
+// entries: 4 / 6 / 8 hops 0.663-0.665 / 0.664-0.665 / 0.738 ms, profiles/r07p_lvl_ab.txt; final tree:
+// 2 / 3 / 5 hops 0.677-0.679 / 0.631-0.635 / 0.626-0.632 against 0.622-0.624 ms, profiles/r09l_lvl_ab.txt)
 #ifndef LVL_HOPS
 #define LVL_HOPS 4
 #endif
