@@ -994,7 +994,9 @@ __global__ void k_lvl_async_final(uint32_t V, const uint32_t *__restrict__ ctl, 
 // could need (ceil(bits(V + 1) / CS_BITS)) and reads nothing back: config 5's 509 levels take one
 // pass and the others return at once.
 // tiles of 16384 keys: config 5's 1M keys are 62 workgroups; 4096 / 8192 / 12288-key tiles ran
-// 0.693-0.699 / 0.653-0.656 / 0.651-0.660 ms against 0.653-0.656 (profiles/r07r_lvl_ab.txt)
+// 0.693-0.699 / 0.653-0.656 / 0.651-0.660 ms against 0.653-0.656 (profiles/r07r_lvl_ab.txt); with the
+// fused late passes 8192 (128 register tiles) / 24576 / 32768 keys 0.634-0.635 / 0.630 / 0.633-0.635
+// against 0.624 ms (profiles/r09m_lvl_ab.txt)
 #ifndef CS_TILE_KEYS
 #define CS_TILE_KEYS 16384
 #endif
