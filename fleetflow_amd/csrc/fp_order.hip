@@ -250,7 +250,7 @@ constexpr uint32_t kInitClaims = kAsyncBlocks / kShards * 64u;  // slots per sha
 #ifndef LVL_SLEEP_LONG
 #define LVL_SLEEP_LONG 8  // s_sleep of an idle wave after LVL_IDLE_SPIN short (s_sleep 1) rounds (2 / 32: +-1 %, r07k)
 #endif
-#ifndef LVL_IDLE_SPIN
+#ifndef LVL_IDLE_SPIN  // final tree: 4 / 64 short rounds, long sleep 4: all within +-0.5 % (profiles/r09n_lvl_ab.txt)
 #define LVL_IDLE_SPIN 16
 #endif
 
